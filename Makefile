@@ -1,0 +1,26 @@
+# Builds the gfx950 kernel library behind the C ABI in include/vda.h.
+#   make            -> video-depth-anything_amd/libvda.so
+#   make oracle     -> nothing to compile (the oracle is a torch-CPU restatement), kept for symmetry
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+PKG     := video-depth-anything_amd
+SRCS    := $(wildcard $(PKG)/csrc/*.hip)
+OBJS    := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(SRCS))
+CXXFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -I include -munsafe-fp-atomics
+
+all: $(PKG)/libvda.so
+
+build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h include/vda.h
+	@mkdir -p build
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(PKG)/libvda.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+
+tools/mfma_probe: tools/mfma_probe.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O2 -Wno-unused-result $< -o $@
+
+clean:
+	rm -rf build $(PKG)/libvda.so
+
+.PHONY: all clean

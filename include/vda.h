@@ -1,0 +1,162 @@
+/*
+ * libvda — MI355X (gfx950) kernels for the Video-Depth-Anything clip forward.
+ *
+ * C ABI: plain pointers, sizes and a hipStream_t passed as void*.  No torch types cross this
+ * boundary; the Python host (video-depth-anything_amd/) hands in device pointers it owns.
+ * Every entry point returns 0 on success, a negative errno-style code for an invalid argument
+ * (-22) or a positive hipError_t for a launch failure; vda_last_error() returns the message.
+ * Nothing here throws, allocates device memory or synchronises the stream, so every call can be
+ * captured into a hipGraph.
+ *
+ * Conventions
+ *   half   = IEEE fp16 (_Float16), float = fp32.
+ *   Activations are token-major / NHWC: a [BT, h, w, C] feature map is a [BT*h*w, C] matrix.
+ *   Linear / conv weights are fp16, K (input channel) contiguous; biases are fp32.
+ *
+ * The reference (FriedFeid/Video-Depth-Anything @ /root/reference) has no native layer or FFI:
+ * its hot path is PyTorch modules.  Each entry point below names the reference code it replaces.
+ */
+#ifndef VDA_H
+#define VDA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Epilogue activation codes for vda_gemm / vda_conv2d. */
+enum {
+  VDA_ACT_NONE = 0,
+  VDA_ACT_GELU = 1,  /* exact erf GELU (nn.GELU, dinov2.py:61 act_layer)                 */
+  VDA_ACT_GEGLU = 2, /* h * gelu(g); weight rows interleaved in 16-row blocks [h|g]      */
+  VDA_ACT_RELU = 3
+};
+
+/* Store layouts for vda_gemm. */
+enum {
+  VDA_STORE_ROWS = 0,         /* Y[m*ldy + n]                                            */
+  VDA_STORE_PIXEL_SHUFFLE = 1 /* ConvTranspose2d(k=s): n=(i*k+j)*Cout+co scattered to NHWC */
+};
+
+/*
+ * Fused epilogue of a GEMM / conv tile, applied to the fp32 accumulator `acc` of output (m, n):
+ *   v = acc + bias[n] + rowbias[((m / rdiv) % rmod) * N + n]
+ *   v = act(v)
+ *   v = res[m*ldres + n] + res2[m*ldres2 + n] + gamma[n] * v      (each term optional)
+ * then stored as fp16.  Null pointers disable a term.  With VDA_ACT_GEGLU the GEMM N counts the
+ * interleaved [h|g] weight rows and the output has N/2 columns.
+ */
+typedef struct vda_epilogue {
+  const float* bias;     /* [N] or NULL                                                */
+  const float* rowbias;  /* [rmod, N] or NULL (patch-embed pos-embed, temporal PE·Wᵀ)  */
+  int32_t rdiv, rmod;
+  const float* gamma;    /* [N] LayerScale or NULL                                     */
+  const void* res;       /* half [M, ldres] or NULL (may alias the output)             */
+  int64_t ldres;
+  const void* res2;      /* half [M, ldres2] or NULL                                   */
+  int64_t ldres2;
+  int32_t act;           /* VDA_ACT_*                                                  */
+  int32_t store;         /* VDA_STORE_*                                                */
+  int32_t ps_k, ps_cout, ps_hin, ps_win; /* pixel-shuffle geometry (store == 1)       */
+} vda_epilogue;
+
+/* Version / diagnostics. */
+const char* vda_version(void);
+const char* vda_last_error(void);
+
+/*
+ * Y[M, N] = epilogue( X[M, K] · W[N, K]ᵀ ).   fp16 in/out, fp32 accumulate, MFMA 16x16x32.
+ * Replaces every nn.Linear / 1x1 nn.Conv2d / ConvTranspose2d(k=s) of the hot path:
+ *   dinov2_layers/attention.py:72,79 (qkv, proj); mlp.py:36-39 (fc1+GELU, fc2); block.py:84-87
+ *   (ls1/ls2 LayerScale + residual); dpt.py:60-68 (projects), dpt.py:70-82 (ConvT k4s4/k2s2);
+ *   blocks.py:124-126,160 (out_conv); motion_module.py:119,127 (proj_in/out + residual);
+ *   motion_module.py:263,272-273 (to_q/k/v with the PE add :256 folded as a per-frame rowbias);
+ *   attention.py:328 (to_out); attention.py:374-384 (GEGLU) and :338 (ff out).
+ * Requires K % 8 == 0, ldx % 8 == 0, N % 4 == 0 (N % 32 == 0 for GEGLU).
+ */
+int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy,
+             int32_t M, int32_t N, int32_t K, const vda_epilogue* epi, void* stream);
+
+/*
+ * NHWC implicit-GEMM 2-D convolution, fp16 MFMA, square kernel `ks`, zero padding `pad`.
+ * X [BT, H, W, Cin] half; Wt [Cout, ks, ks, Cin] half; Y [BT, Ho, Wo, Cout] half.
+ * pre_relu applies ReLU to X as it is loaded (ResidualConvUnit, blocks.py:78).
+ * Replaces blocks.py:20-32 (layerN_rn 3x3 no bias), blocks.py:78-91 (RCU conv1/conv2 + skip
+ * add), blocks.py:146-150 (fusion skip add, via res2), dpt.py:83-89 (3x3 s2 resize), and
+ * dpt.py:117 (output_conv1).  Requires Cin % 8 == 0, Cout % 4 == 0.
+ * If `up_h`/`up_w` > 0, X is read through a bilinear align_corners=True upsample from
+ * [BT, H, W, Cin] to [BT, up_h, up_w, Cin] (blocks.py:156-158 / dpt_temporal.py:92-94), and the
+ * conv runs on the upsampled grid.
+ */
+int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
+               int32_t Cin, int32_t Cout, int32_t ks, int32_t stride, int32_t pad,
+               int32_t pre_relu, int32_t up_h, int32_t up_w, const vda_epilogue* epi, void* stream);
+
+/*
+ * Row LayerNorm, fp32 statistics.  X rows of C halfs (row stride ldx); Y [rows, C] half.
+ * With skip_period > 0, output row r reads input row r + r/(skip_period) + 1, i.e. it drops the
+ * cls token of every [1+skip_period]-token frame (dinov2.py:309-312).
+ * Replaces block.py:84,87 (norm1/norm2, eps 1e-6), dinov2.py:310 (final norm on the taps),
+ * motion_module.py:175,183 (temporal LayerNorms, eps 1e-5).
+ */
+int vda_layernorm(const void* x, int64_t ldx, void* y, const float* gamma, const float* beta,
+                  int32_t rows, int32_t C, float eps, int32_t skip_period, void* stream);
+
+/*
+ * GroupNorm over NHWC frames: X [F, S, C] half -> Y [F, S, C] half, `groups` groups of C/groups
+ * channels, statistics over (S x C/groups) in fp32.  `ws` is a float workspace of >= 2*F*groups
+ * entries.  Replaces motion_module.py:116 (GroupNorm(32, eps 1e-6)).
+ */
+int vda_groupnorm(const void* x, void* y, const float* gamma, const float* beta, int32_t F,
+                  int32_t S, int32_t C, int32_t groups, float eps, float* ws, void* stream);
+
+/*
+ * Spatial multi-head self-attention (flash / online softmax, fp16 MFMA, fp32 softmax).
+ * qkv [B*N, 3*H*D] half laid out as [B, N, 3, H, D] (the nn.Linear qkv output);
+ * out [B*N, H*D] half.  D must be 64.  Replaces dinov2_layers/attention.py:49-62/:65-81
+ * (softmax(q kᵀ / sqrt(D)) v; xformers memory_efficient_attention BMHK).
+ */
+int vda_spatial_attention(const void* qkv, void* out, int32_t B, int32_t N, int32_t H,
+                          int32_t D, float scale, void* stream);
+
+/*
+ * Temporal self-attention across T <= 32 frames at every spatial site.
+ * qkv [(B*T)*S, 3*H*D] half (frame-major rows, [q|k|v] columns, heads contiguous);
+ * out [(B*T)*S, H*D] half.  D % 8 == 0, D <= 128.
+ * Replaces motion_module.py:247-335 (rearrange (b f) d c -> (b d) f c, 8-head softmax over f,
+ * rearrange back) and attention.py:182-211/:256-293.
+ */
+int vda_temporal_attention(const void* qkv, void* out, int32_t B, int32_t T, int32_t S,
+                           int32_t H, int32_t D, float scale, void* stream);
+
+/*
+ * Bilinear resize, align_corners=True, NHWC half: X [BT, H, W, C] -> Y [BT, Ho, Wo, C].
+ * Replaces blocks.py:156-158 and dpt_temporal.py:92-94 where not fused into a conv.
+ */
+int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t H, int32_t W, int32_t C,
+                          int32_t Ho, int32_t Wo, void* stream);
+
+/*
+ * Patch-embed im2col: images [BT, 3, H, W] float (NCHW, as VideoDepthAnything.forward receives
+ * them) -> A [BT*(1+np), Kp] half with np = (H/14)*(W/14), K order (ci, ky, kx), zero-padded to
+ * Kp >= 588, and an all-zero row 0 per frame for the cls token.  Followed by vda_gemm with a
+ * per-token rowbias this replaces patch_embed.py:69-82 + dinov2.py:212-219 (cls cat, pos add).
+ */
+int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W, int32_t Kp,
+                     void* stream);
+
+/*
+ * Depth head tail in fp32 (dpt_temporal.py:92-99, dpt.py:118-124, video_depth.py:63-64):
+ * X [BT, Hin, Win, C] half (output_conv1 result) is bilinearly resized (align_corners=True) to
+ * [Ho, Wo], then conv3x3(C->32, w1 [32,3,3,C] float, b1) -> ReLU -> conv1x1(32->1, w2 [32], b2)
+ * -> ReLU, all in fp32.  depth [BT, Ho, Wo] float.  C % 8 == 0, C <= 256.
+ */
+int vda_depth_head(const void* x, const float* w1, const float* b1, const float* w2,
+                   const float* b2, float* depth, int32_t BT, int32_t Hin, int32_t Win,
+                   int32_t C, int32_t Ho, int32_t Wo, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VDA_H */

@@ -1,0 +1,218 @@
+"""Per-kernel parity: each libvda entry point (through the C ABI) vs a torch fp32 CPU reference.
+
+Tolerances are stated per test; they cover fp16 storage of inputs/outputs with fp32 accumulation.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import vda_amd
+from vda_amd import ops
+from vda_amd._lib import ACT_GELU, ACT_GEGLU, ACT_RELU
+from vda_amd.model import _geglu_interleave
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).abs().sum() / b.abs().sum().clamp_min(1e-30))
+
+
+def h(t):
+    return t.to(DEV, torch.float16).contiguous()
+
+
+def f32(t):
+    return t.to(DEV, torch.float32).contiguous()
+
+
+def rnd(*s, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*s, generator=g) * scale).half().float()
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 384, 200), (128, 128, 64), (1370, 1152, 384), (77, 64, 96), (5, 48, 8),
+                                   (4000, 3072, 1024)])
+def test_gemm_bias(M, N, K):
+    x, w, b = rnd(M, K, seed=1), rnd(N, K, scale=K ** -0.5, seed=2), rnd(N, scale=0.1, seed=3)
+    y = ops.gemm(h(x), h(w), bias=f32(b))
+    ref = x @ w.t() + b
+    assert rel(y, ref) < 2e-3  # fp16 output rounding
+
+
+def test_gemm_gelu_ls_residual_rowbias():
+    M, N, K = 700, 256, 320
+    x, w, b = rnd(M, K, seed=4), rnd(N, K, scale=K ** -0.5, seed=5), rnd(N, scale=0.1, seed=6)
+    gam, res = rnd(N, seed=7).abs() + 0.1, rnd(M, N, seed=8)
+    y = ops.gemm(h(x), h(w), bias=f32(b), act=ACT_GELU)
+    assert rel(y, F.gelu(x @ w.t() + b)) < 2e-3
+    r = h(res)
+    ops.gemm(h(x), h(w), bias=f32(b), gamma=f32(gam), res=r, out=r)  # in place, like the encoder
+    assert rel(r, res + gam * (x @ w.t() + b)) < 2e-3
+    T, S = 7, 100
+    rb = rnd(T, N, seed=9)
+    y = ops.gemm(h(x), h(w), rowbias=f32(rb), rdiv=S, rmod=T)
+    ref = x @ w.t() + rb[(torch.arange(M) // S) % T]
+    assert rel(y, ref) < 2e-3
+
+
+def test_gemm_geglu():
+    M, C = 333, 64
+    x = rnd(M, C, seed=10)
+    w = rnd(8 * C, C, scale=C ** -0.5, seed=11)
+    b = rnd(8 * C, scale=0.1, seed=12)
+    y = ops.gemm(h(x), h(_geglu_interleave(w)), bias=f32(_geglu_interleave(b)), act=ACT_GEGLU)
+    hh, g = (x @ w.t() + b).chunk(2, -1)
+    assert rel(y, hh * F.gelu(g)) < 2e-3
+
+
+def test_gemm_strided_rows():
+    M, N, K = 200, 128, 128
+    big = rnd(M, 3 * K, seed=13)
+    w = rnd(N, K, scale=K ** -0.5, seed=14)
+    y = ops.gemm(h(big)[:, K:2 * K], h(w))
+    assert rel(y, big[:, K:2 * K] @ w.t()) < 2e-3
+
+
+@pytest.mark.parametrize("k,cin,cout", [(4, 48, 48), (2, 96, 96), (4, 256, 256)])
+def test_conv_transpose_pixel_shuffle(k, cin, cout):
+    BT, hh, ww = 3, 5, 7
+    x = rnd(BT, cin, hh, ww, seed=15)
+    w = rnd(cin, cout, k, k, scale=cin ** -0.5, seed=16)
+    b = rnd(cout, scale=0.1, seed=17)
+    ref = F.conv_transpose2d(x, w, b, stride=k).permute(0, 2, 3, 1)
+    wp = w.permute(2, 3, 1, 0).reshape(k * k * cout, cin)
+    y = ops.conv_transpose_ks(h(x.permute(0, 2, 3, 1).reshape(-1, cin)), h(wp), f32(b.repeat(k * k)), BT, hh, ww, k)
+    assert rel(y, ref) < 2e-3
+
+
+@pytest.mark.parametrize("cin,cout,stride,H,W", [(64, 64, 1, 9, 11), (48, 64, 1, 12, 12), (256, 256, 1, 19, 19),
+                                                 (384, 384, 2, 9, 9), (1024, 256, 1, 5, 5), (96, 32, 1, 3, 4)])
+def test_conv3x3(cin, cout, stride, H, W):
+    BT = 2
+    x = rnd(BT, cin, H, W, seed=18)
+    w = rnd(cout, cin, 3, 3, scale=(9 * cin) ** -0.5, seed=19)
+    b = rnd(cout, scale=0.1, seed=20)
+    ref = F.conv2d(x, w, b, stride=stride, padding=1)
+    y = ops.conv2d(h(x.permute(0, 2, 3, 1)), h(w.permute(0, 2, 3, 1)), stride=stride, bias=f32(b))
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 2e-3
+
+
+def test_conv3x3_rcu_fusion_epilogue():
+    """out = x0 + conv2(relu(conv1(relu(x1)))) + x1  (blocks.py:78-91, :146-150)."""
+    BT, C, H, W = 2, 64, 10, 13
+    x0, x1 = rnd(BT, C, H, W, seed=21), rnd(BT, C, H, W, seed=22)
+    w1, w2 = rnd(C, C, 3, 3, scale=(9 * C) ** -0.5, seed=23), rnd(C, C, 3, 3, scale=(9 * C) ** -0.5, seed=24)
+    b1, b2 = rnd(C, scale=0.1, seed=25), rnd(C, scale=0.1, seed=26)
+    t = F.relu(F.conv2d(F.relu(x1), w1, b1, padding=1))
+    ref = F.conv2d(t, w2, b2, padding=1) + x1 + x0
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    tt = ops.conv2d(nh(x1), nh(w1), bias=f32(b1), pre_relu=True, act=ACT_RELU)
+    y = ops.conv2d(tt, nh(w2), bias=f32(b2), res=nh(x1), res2=nh(x0))
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 3e-3
+
+
+def test_conv3x3_fused_upsample():
+    BT, C, H, W = 2, 64, 7, 9
+    x = rnd(BT, C, H, W, seed=27)
+    w = rnd(32, C, 3, 3, scale=(9 * C) ** -0.5, seed=28)
+    b = rnd(32, scale=0.1, seed=29)
+    up = F.interpolate(x, size=(14, 18), mode="bilinear", align_corners=True)
+    ref = F.conv2d(up, w, b, padding=1)
+    y = ops.conv2d(h(x.permute(0, 2, 3, 1)), h(w.permute(0, 2, 3, 1)), bias=f32(b), up=(14, 18))
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 3e-3
+
+
+@pytest.mark.parametrize("C", [384, 1024, 256, 64])
+def test_layernorm(C):
+    R = 517
+    x = rnd(R, C, seed=30) * 2 + 0.5
+    g, b = rnd(C, seed=31) * 0.1 + 1, rnd(C, seed=32) * 0.1
+    y = ops.layernorm(h(x), f32(g), f32(b), 1e-6)
+    assert rel(y, F.layer_norm(x, (C,), g, b, eps=1e-6)) < 2e-3
+
+
+def test_layernorm_skip_cls():
+    BT, np_, C = 3, 10, 384
+    x = rnd(BT, np_ + 1, C, seed=33)
+    g, b = rnd(C, seed=34) * 0.1 + 1, rnd(C, seed=35) * 0.1
+    y = ops.layernorm(h(x.reshape(-1, C)), f32(g), f32(b), 1e-6, skip_period=np_)
+    ref = F.layer_norm(x, (C,), g, b, eps=1e-6)[:, 1:].reshape(-1, C)
+    assert rel(y, ref) < 2e-3
+
+
+@pytest.mark.parametrize("C,S", [(1024, 50), (256, 70), (384, 33), (64, 90)])
+def test_groupnorm(C, S):
+    Fr = 3
+    x = rnd(Fr, S, C, seed=36) + 0.3
+    g, b = rnd(C, seed=37) * 0.1 + 1, rnd(C, seed=38) * 0.1
+    y = ops.groupnorm(h(x.reshape(-1, C)), f32(g), f32(b), Fr, 32, 1e-6)
+    ref = F.group_norm(x.permute(0, 2, 1), 32, g, b, eps=1e-6).permute(0, 2, 1).reshape(-1, C)
+    assert rel(y, ref) < 2e-3
+
+
+@pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1)])
+def test_spatial_attention(B, N, H):
+    D = 64
+    qkv = rnd(B * N, 3 * H * D, seed=39)
+    y = ops.spatial_attention(h(qkv), B, N, H, D)
+    q, k, v = qkv.reshape(B, N, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = ((q @ k.transpose(-1, -2)) * D ** -0.5).softmax(-1) @ v
+    ref = ref.transpose(1, 2).reshape(B * N, H * D)
+    assert rel(y, ref) < 3e-3
+
+
+@pytest.mark.parametrize("B,T,S,D", [(1, 32, 37, 128), (1, 8, 10, 32), (2, 5, 9, 48), (1, 32, 20, 8), (1, 3, 4, 24)])
+def test_temporal_attention(B, T, S, D):
+    H = 8
+    C = H * D
+    qkv = rnd(B * T * S, 3 * C, seed=40) * 2
+    y = ops.temporal_attention(h(qkv), B, T, S, H, D)
+    t = qkv.reshape(B, T, S, 3, H, D).permute(3, 0, 2, 4, 1, 5)  # 3, B, S, H, T, D
+    q, k, v = t[0], t[1], t[2]
+    o = ((q @ k.transpose(-1, -2)) * D ** -0.5).softmax(-1) @ v  # B, S, H, T, D
+    ref = o.permute(0, 3, 1, 2, 4).reshape(B * T * S, C)
+    assert rel(y, ref) < 3e-3
+
+
+def test_upsample_bilinear():
+    x = rnd(2, 32, 19, 19, seed=41)
+    ref = F.interpolate(x, size=(37, 37), mode="bilinear", align_corners=True)
+    y = ops.upsample_bilinear(h(x.permute(0, 2, 3, 1)), 37, 37)
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 2e-3
+
+
+def test_patch_embed_im2col_gemm():
+    BT, H, W, C = 2, 42, 56, 64
+    img = rnd(BT, 3, H, W, seed=42)
+    w = rnd(C, 3, 14, 14, scale=588 ** -0.5, seed=43)
+    b = rnd(C, scale=0.1, seed=44)
+    ref = F.conv2d(img, w, b, stride=14).flatten(2).transpose(1, 2)  # [BT, np, C]
+    a = ops.patch_im2col(img.to(DEV).contiguous(), 592)
+    wp = F.pad(w.reshape(C, -1), (0, 4))
+    np_ = (H // 14) * (W // 14)
+    rb = torch.cat([torch.zeros(1, C), b.expand(np_, C)], 0)
+    y = ops.gemm(a, h(wp), rowbias=f32(rb), rdiv=1, rmod=np_ + 1).view(BT, np_ + 1, C)
+    assert float(y[:, 0].abs().max()) == 0.0
+    assert rel(y[:, 1:], ref) < 2e-3
+
+
+def test_depth_head_fp32():
+    BT, C, Hin, Win, Ho, Wo = 2, 32, 16, 20, 28, 42
+    x = rnd(BT, C, Hin, Win, seed=45)
+    w1, b1 = rnd(32, C, 3, 3, scale=(9 * C) ** -0.5, seed=46), rnd(32, scale=0.1, seed=47)
+    w2, b2 = rnd(1, 32, 1, 1, seed=48).abs() * 0.2, torch.tensor([0.05])
+    up = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=True)
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(up, w1, b1, padding=1)), w2, b2))[:, 0]
+    y = ops.depth_head(h(x.permute(0, 2, 3, 1)), f32(w1.permute(0, 2, 3, 1)), f32(b1), f32(w2.reshape(-1)), f32(b2),
+                       Ho, Wo)
+    assert rel(y, ref) < 1e-5  # fp32 path on fp16-exact inputs
+
+
+def test_ops_reject_cpu_tensors():
+    with pytest.raises(RuntimeError):
+        ops.gemm(torch.zeros(4, 8, dtype=torch.float16), torch.zeros(4, 8, dtype=torch.float16))

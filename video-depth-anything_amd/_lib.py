@@ -1,0 +1,94 @@
+"""ctypes binding of libvda.so (the C ABI declared in include/vda.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) and loaded from this
+package directory.  There is no fallback: if the library is missing or fails to load, every op
+raises ``VDAUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int32, c_int64, c_void_p, POINTER
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvda.so")
+
+# Every symbol include/vda.h declares (checked by tests/test_capi.py).
+EXPORTED = (
+    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm",
+    "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
+    "vda_depth_head",
+)
+
+ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
+STORE_ROWS, STORE_PIXEL_SHUFFLE = 0, 1
+
+
+class VDAUnavailable(RuntimeError):
+    pass
+
+
+class VDAError(RuntimeError):
+    pass
+
+
+class Epilogue(ctypes.Structure):
+    """Mirror of ``vda_epilogue`` (include/vda.h)."""
+    _fields_ = [
+        ("bias", c_void_p), ("rowbias", c_void_p), ("rdiv", c_int32), ("rmod", c_int32),
+        ("gamma", c_void_p), ("res", c_void_p), ("ldres", c_int64), ("res2", c_void_p),
+        ("ldres2", c_int64), ("act", c_int32), ("store", c_int32), ("ps_k", c_int32),
+        ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
+    ]
+
+
+_lib = None
+_load_error = None
+
+
+def _declare(lib):
+    P, I, L, F = c_void_p, c_int32, c_int64, c_float
+    EP = POINTER(Epilogue)
+    sig = {
+        "vda_version": ([], ctypes.c_char_p),
+        "vda_last_error": ([], ctypes.c_char_p),
+        "vda_gemm": ([P, L, P, P, L, I, I, I, EP, P], I),
+        "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P], I),
+        "vda_layernorm": ([P, L, P, P, P, I, I, F, I, P], I),
+        "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
+        "vda_spatial_attention": ([P, P, I, I, I, I, F, P], I),
+        "vda_temporal_attention": ([P, P, I, I, I, I, I, F, P], I),
+        "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),
+        "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
+        "vda_depth_head": ([P, P, P, P, P, P, I, I, I, I, I, I, P], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def lib():
+    """Return the loaded libvda (raises VDAUnavailable if it cannot be loaded)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise VDAUnavailable(_load_error)
+    if not os.path.exists(LIB_PATH):
+        _load_error = f"libvda.so not found at {LIB_PATH}; run `make` (or __graft_entry__.build())"
+        raise VDAUnavailable(_load_error)
+    try:
+        l = ctypes.CDLL(LIB_PATH)
+        _declare(l)
+    except OSError as e:  # pragma: no cover - depends on the runtime
+        _load_error = f"failed to load {LIB_PATH}: {e}"
+        raise VDAUnavailable(_load_error) from e
+    _lib = l
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().vda_last_error().decode(errors="replace")
+        raise VDAError(f"{what} failed (rc={rc}): {msg}")

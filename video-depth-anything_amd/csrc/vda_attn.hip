@@ -1,0 +1,323 @@
+// Spatial (DINOv2) and temporal (motion-module) attention, fp16 MFMA + fp32 online softmax.
+#include "vda_common.h"
+#include "../../include/vda.h"
+
+namespace {
+
+// =============================================================================================
+// Spatial attention, D = 64.  Block = 4 waves x 32 queries = 128 queries of one (batch, head);
+// key/value tiles of 64 rows are staged in LDS (register-staged double buffer).
+//
+// Everything is computed transposed so that a lane owns ONE query column:
+//   Sᵀ = K · Qᵀ     (A = K rows from LDS, B = Q rows held in registers)   -> lane: 16 keys of q
+//   Oᵀ += Vᵀ · Pᵀ   (A = Vᵀ via ds_read_b64_tr_b16 from the row-major V tile, B = P from regs)
+// The Pᵀ accumulator feeds the PV MFMA directly: lane group g holds keys {4g..4g+3} of each
+// 16-key subtile, so the PV k-order is permuted identically on the Vᵀ side (two tr reads per
+// fragment, rows kc*32+4g.. and kc*32+16+4g..).  Oᵀ lanes hold 4 consecutive head channels of
+// one query -> 8-byte output stores and per-lane softmax rescale, no cross-lane traffic except
+// the 4-lane max/sum reductions.
+// =============================================================================================
+constexpr int SD = 64;       // head dim
+constexpr int SQB = 128;     // queries per block
+constexpr int SKB = 64;      // keys per tile
+
+__device__ __forceinline__ int k_swz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
+__device__ __forceinline__ int v_swz(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 1) & 3) << 1)) << 3); }
+
+__global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                           int N, int H, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) h16 sK[2][SKB * SD];
+  __shared__ __attribute__((aligned(16))) h16 sV[2][SKB * SD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int C = H * SD;
+  const long ld = 3L * C;
+  const h16* base = qkv + (long)b * N * ld;
+  const int g = lane >> 4, li = lane & 15;
+
+  // Q fragments: B operand, lane holds Q[q = qs*16 + li][d = ks*32 + 8g .. +7]
+  h8 qf[2][2];
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    const int q = blockIdx.x * SQB + wave * 32 + qs * 16 + li;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (q < N) qf[qs][ks] = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + h * SD + ks * 32 + g * 8));
+      else qf[qs][ks] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+
+  f4 o[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) o[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.f, 0.f};
+
+  // staging: each thread moves 2 K chunks and 2 V chunks (16 B) per tile
+  const int srow = tid >> 3, schunk = tid & 7;
+  uint4 rk[2], rv[2];
+  auto gload = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int key = kt * SKB + srow + 32 * i;
+      if (key < N) {
+        const h16* rp = base + (long)key * ld + h * SD + schunk * 8;
+        rk[i] = ldg16(rp + C);
+        rv[i] = ldg16(rp + 2 * C);
+      } else {
+        rk[i] = make_uint4(0, 0, 0, 0);
+        rv[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<uint4*>(&sK[buf][k_swz(srow + 32 * i, schunk)]) = rk[i];
+      *reinterpret_cast<uint4*>(&sV[buf][v_swz(srow + 32 * i, schunk)]) = rv[i];
+    }
+  };
+
+  const int ntiles = (N + SKB - 1) / SKB;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < ntiles) gload(kt + 1);
+
+    // ---- Sᵀ = K Qᵀ : s[kt4][qs] lane holds keys kt4*16 + 4g + r, query qs*16 + li
+    f4 s[4][2];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) s[a][qs] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const h8 kf = *reinterpret_cast<const h8*>(&sK[buf][k_swz(a * 16 + li, ks * 4 + g)]);
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) s[a][qs] = mfma16(kf, qf[qs][ks], s[a][qs]);
+      }
+    }
+    // ---- online softmax (base-2), mask keys >= N
+    const int kbase = kt * SKB;
+    const bool tail = kbase + SKB > N;
+    h8 pf[2][2];  // [qs][kc] P fragments (B operand of PV)
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = s[a][qs][r] * scale_log2;
+          if (tail && kbase + a * 16 + 4 * g + r >= N) t = -INFINITY;
+          s[a][qs][r] = t;
+          mx = fmaxf(mx, t);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mnew = fmaxf(mrun[qs], mx);
+      const float alpha = exp2f(mrun[qs] - mnew);
+      mrun[qs] = mnew;
+      float ps = 0.f;
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float pv = exp2f(s[a][qs][r] - mnew);
+          ps += pv;
+          pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)pv;
+        }
+      lrun[qs] = lrun[qs] * alpha + ps;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) o[d][qs] *= alpha;
+    }
+    // ---- Oᵀ += Vᵀ Pᵀ
+#pragma unroll
+    for (int kc = 0; kc < 2; ++kc) {
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        // lane 4q+p of group g: row kc*32 + 4g + q, cols d*16 + 4p
+        const int q4 = li >> 2, p4 = li & 3;
+        const int col = d * 16 + 4 * p4;
+        const int r0 = kc * 32 + 4 * g + q4, r1 = r0 + 16;
+        const h4 v0 = lds_read_tr16(&sV[buf][v_swz(r0, col >> 3) + (col & 7)]);
+        const h4 v1 = lds_read_tr16(&sV[buf][v_swz(r1, col >> 3) + (col & 7)]);
+        const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+        for (int qs = 0; qs < 2; ++qs) o[d][qs] = mfma16(vf, pf[qs][kc], o[d][qs]);
+      }
+    }
+    if (kt + 1 < ntiles) sstore(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- epilogue: normalise and store (lane: d = dsub*16 + 4g + r, q = qs*16 + li)
+#pragma unroll
+  for (int qs = 0; qs < 2; ++qs) {
+    float l = lrun[qs];
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    const float inv = 1.f / l;
+    const int q = blockIdx.x * SQB + wave * 32 + qs * 16 + li;
+    if (q < N) {
+      h16* op = out + ((long)b * N + q) * C + h * SD;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        h4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (h16)(o[d][qs][r] * inv);
+        *reinterpret_cast<h4*>(op + d * 16 + 4 * g) = v;
+      }
+    }
+  }
+}
+
+// =============================================================================================
+// Temporal attention: one wave per (batch, site s, head), T <= 32 frames, v_mfma_f32_32x32x16_f16.
+//   Sᵀ[key][q] = Σ_d K[key][d] Q[q][d]       A = K rows, B = Q rows (fragments straight from HBM)
+//   Oᵀ[d][q]   = Σ_key Vᵀ[d][key] Pᵀ[key][q]  B = Pᵀ accumulator registers 8s..8s+7 (k order
+//                16s + 8(j>>2) + 4h + (j&3)), A = Vᵀ by ds_read_b64_tr_b16 from a per-wave V tile.
+// DP = head dim padded to a multiple of 16 (zero-filled), NDT = 32-wide output d tiles.
+// =============================================================================================
+template <int DP>
+__global__ __launch_bounds__(256) void temporal_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                            int B, int T, int S, int H, int D, float scale_log2) {
+  constexpr int NST = DP / 16;
+  constexpr int NDT = (DP + 31) / 32;
+  constexpr int DP32 = NDT * 32;
+  constexpr int VSTR = DP32 + (DP32 > 32 ? 32 : 0);  // row stride (halfs) of the V tile
+  __shared__ __attribute__((aligned(16))) h16 sV[4][32 * VSTR];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long item = (long)blockIdx.x * 4 + wave;
+  const long nitems = (long)B * S * H;
+  const bool active = item < nitems;
+  const int hh = active ? (int)(item % H) : 0;
+  const long bs = active ? item / H : 0;
+  const int s = (int)(bs % S), b = (int)(bs / S);
+  const int C = H * D;
+  const long ld = 3L * C;
+  const int r32 = lane & 31, hf = lane >> 5;
+  h16* vt = sV[wave];
+
+  // V tile -> LDS (rows = keys, zero beyond T / D)
+  {
+    constexpr int CPR = DP32 / 8;  // 16-B chunks per row
+    for (int i = lane; i < 32 * CPR; i += 64) {
+      const int key = i / CPR, ch = i - key * CPR;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (active && key < T && ch * 8 < D)
+        v = ldg16(qkv + ((long)(b * T + key) * S + s) * ld + 2 * C + hh * D + ch * 8);
+      *reinterpret_cast<uint4*>(vt + key * VSTR + ch * 8) = v;
+    }
+  }
+  // Sᵀ
+  f16x acc = {};
+  const long krow = ((long)(b * T + r32) * S + s) * ld + hh * D;
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    const int d0 = st * 16 + hf * 8;
+    h8 kf = h8{0, 0, 0, 0, 0, 0, 0, 0}, qf = kf;
+    if (active && r32 < T && d0 < D) {
+      qf = __builtin_bit_cast(h8, ldg16(qkv + krow + d0));
+      kf = __builtin_bit_cast(h8, ldg16(qkv + krow + C + d0));
+    }
+    acc = mfma32(kf, qf, acc);
+  }
+  // softmax over keys (lane holds keys (r&3)+8(r>>2)+4hf for query r32; partner lane^32 the rest)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    float t = acc[r] * scale_log2;
+    if (key >= T) t = -INFINITY;
+    acc[r] = t;
+    mx = fmaxf(mx, t);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+  h8 pf[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = exp2f(acc[r] - mx);
+    sum += p;
+    pf[r >> 3][r & 7] = (h16)p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  __syncthreads();  // V tile visible to the whole wave (all waves reach this)
+
+  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    f16x o = {};
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      // tr16 read: group grp -> key rows 16st + 4*(grp>>1) + q4 (+8), cols dt*32 + (grp&1)*16 + 4p4
+      const int col = dt * 32 + (grp & 1) * 16 + 4 * p4;
+      const int r0 = 16 * st + 4 * (grp >> 1) + q4;
+      const h4 v0 = lds_read_tr16(vt + r0 * VSTR + col);
+      const h4 v1 = lds_read_tr16(vt + (r0 + 8) * VSTR + col);
+      const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      o = mfma32(vf, pf[st], o);
+    }
+    // lane holds Oᵀ[d = dt*32 + (r&3) + 8(r>>2) + 4hf][q = r32]
+    if (active && r32 < T) {
+      h16* op = out + ((long)(b * T + r32) * S + s) * C + hh * D;
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        const int d = dt * 32 + 8 * gq + 4 * hf;
+        if (d < D) {
+          h4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (h16)(o[gq * 4 + r] * inv);
+          *reinterpret_cast<h4*>(op + d) = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int32_t N, int32_t H,
+                                     int32_t D, float scale, void* stream) {
+  VDA_CHECK_ARG(qkv && out, "null pointer");
+  VDA_CHECK_ARG(B > 0 && N > 0 && H > 0, "empty attention");
+  VDA_CHECK_ARG(D == SD, "spatial attention supports head dim 64 only");
+  dim3 grid((N + SQB - 1) / SQB, H, B);
+  hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
+                     (h16*)out, N, H, scale * 1.4426950408889634f);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int32_t T, int32_t S,
+                                      int32_t H, int32_t D, float scale, void* stream) {
+  VDA_CHECK_ARG(qkv && out, "null pointer");
+  VDA_CHECK_ARG(B > 0 && S > 0 && H > 0, "empty attention");
+  VDA_CHECK_ARG(T > 0 && T <= 32, "temporal attention needs 1 <= T <= 32 (PE table length)");
+  VDA_CHECK_ARG(D > 0 && D % 8 == 0 && D <= 128, "head dim must be a multiple of 8, <= 128");
+  const long items = (long)B * S * H;
+  dim3 grid((unsigned)((items + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  const float sl = scale * 1.4426950408889634f;
+  const int dp = (D + 15) / 16 * 16;
+#define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl)
+  switch (dp) {
+    case 16: VDA_TA(16); break;
+    case 32: VDA_TA(32); break;
+    case 48: VDA_TA(48); break;
+    case 64: VDA_TA(64); break;
+    case 80: VDA_TA(80); break;
+    case 96: VDA_TA(96); break;
+    case 112: VDA_TA(112); break;
+    default: VDA_TA(128); break;
+  }
+#undef VDA_TA
+  VDA_LAUNCH_CHECK();
+  return 0;
+}

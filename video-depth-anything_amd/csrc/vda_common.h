@@ -1,0 +1,65 @@
+// Shared device helpers for libvda (gfx950 / CDNA4 only).
+//
+// Every hot op of the Video-Depth-Anything clip forward runs through
+// kernels built on these types.  Activations and weights are fp16 in HBM, accumulation and
+// all normalisation / softmax statistics are fp32.  Activations are token-major (NHWC) end
+// to end, so the reference's permute/rearrange calls become index math in the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 h16;
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f16x __attribute__((ext_vector_type(16)));
+
+#define VDA_LDS __attribute__((address_space(3)))
+
+__device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f16x mfma32(h8 a, h8 b, f16x c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+// Hardware-transposed LDS read (ds_read_b64_tr_b16): per 16-lane group, lane 4q+p supplies the
+// address of row q / columns 4p..4p+3 of a 4x16 block; lane i receives column i (4 rows).
+__device__ __forceinline__ h4 lds_read_tr16(const h16* p) {
+  s4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16((VDA_LDS s4*)(p));
+  return __builtin_bit_cast(h4, t);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void stg16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+
+__device__ __forceinline__ uint4 relu_h8(uint4 v) {
+  h8 x = __builtin_bit_cast(h8, v);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = x[j] > (h16)0 ? x[j] : (h16)0;
+  return __builtin_bit_cast(uint4, x);
+}
+
+// Error reporting across the C ABI (never throws).
+int vda_set_error(int code, const char* msg);
+#define VDA_CHECK_ARG(cond, msg) \
+  do { if (!(cond)) return vda_set_error(-22, msg); } while (0)
+#define VDA_LAUNCH_CHECK() \
+  do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return vda_set_error((int)_e, hipGetErrorString(_e)); } while (0)

@@ -1,0 +1,374 @@
+// MFMA GEMM + implicit-GEMM convolution with fused epilogues (gfx950).
+//
+// Y[m, n] = epi( sum_k X[m, k] * W[n, k] ).  One kernel template serves every nn.Linear, 1x1
+// conv, ConvTranspose2d(k=s) and 3x3 conv of the Video-Depth-Anything forward (see include/vda.h
+// for the reference call sites).
+//
+// Tiling: BM x BN block tile, BK = 64, 256 threads = 4 waves as 2 (m) x 2 (n); each wave owns a
+// (BM/2) x (BN/2) sub-tile computed with v_mfma_f32_16x16x32_f16.  The MFMA is issued in the
+// "swapped" orientation: the A operand is a 16-row slice of W (output channels) and the B operand
+// a 16-row slice of X (tokens/pixels), so each lane ends up holding FOUR CONSECUTIVE OUTPUT
+// CHANNELS of one token: the epilogue does 8-byte loads/stores of bias/residual/output and the
+// GEGLU pair (h, g) of a channel lands in the same lane.
+//
+// Staging: register-staged double-buffered LDS (global loads for tile t+1 are issued before the
+// MFMAs of tile t, written to the other LDS buffer after them; one barrier per K tile).  LDS rows
+// are 128 B (64 halfs) with the 16-B chunk index XOR-swizzled by (row>>1)&7, which makes both the
+// ds_write_b128 stores and the 16-lane ds_read_b128 fragment reads bank-conflict free.
+#include "vda_common.h"
+#include "../../include/vda.h"
+
+namespace {
+
+constexpr int BK = 64;
+
+struct GemmParams {
+  const h16* x; long ldx;
+  const h16* w;
+  h16* y; long ldy;
+  int M, N, K;
+  // implicit conv geometry (conv mode only)
+  int H, W, Cin, Ho, Wo, ks, stride, pad, pre_relu, up_h, up_w;
+  vda_epilogue epi;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) {  // half offset in a [rows][64] tile
+  return row * BK + ((chunk ^ ((row >> 1) & 7)) << 3);
+}
+
+// ---- X-tile loaders -------------------------------------------------------------------------
+// Dense: X is a row-major [M, K] matrix with row stride ldx.
+struct DenseLoader {
+  const h16* rowp[4];
+  bool rowok[4];
+  __device__ void init(const GemmParams& p, int m0, int tid, int nrow_iters) {
+    for (int i = 0; i < nrow_iters; ++i) {
+      int r = (tid >> 3) + 32 * i;
+      int m = m0 + r;
+      rowok[i] = m < p.M;
+      rowp[i] = p.x + (long)(rowok[i] ? m : 0) * p.ldx;
+    }
+  }
+  __device__ uint4 load(const GemmParams& p, int i, int k) const {
+    if (rowok[i] && k < p.K) return ldg16(rowp[i] + k);
+    return make_uint4(0, 0, 0, 0);
+  }
+};
+
+// Implicit GEMM conv: row m = output pixel (bt, oy, ox), k = (ky*ks + kx)*Cin + ci.
+struct ConvLoader {
+  int bt[4], oy[4], ox[4];
+  bool rowok[4];
+  __device__ void init(const GemmParams& p, int m0, int tid, int nrow_iters) {
+    for (int i = 0; i < nrow_iters; ++i) {
+      int r = (tid >> 3) + 32 * i;
+      int m = m0 + r;
+      rowok[i] = m < p.M;
+      int mm = rowok[i] ? m : 0;
+      ox[i] = mm % p.Wo;
+      int t = mm / p.Wo;
+      oy[i] = t % p.Ho;
+      bt[i] = t / p.Ho;
+    }
+  }
+  __device__ uint4 load(const GemmParams& p, int i, int k) const {
+    if (!rowok[i] || k >= p.K) return make_uint4(0, 0, 0, 0);
+    int tap = k / p.Cin;
+    int ci = k - tap * p.Cin;
+    int ky = tap / p.ks, kx = tap - ky * p.ks;
+    int iy = oy[i] * p.stride - p.pad + ky;
+    int ix = ox[i] * p.stride - p.pad + kx;
+    uint4 v;
+    if (p.up_h > 0) {
+      // conv input = bilinear(align_corners=True) upsample of the stored [H, W] map to [up_h, up_w]
+      if (iy < 0 || iy >= p.up_h || ix < 0 || ix >= p.up_w) return make_uint4(0, 0, 0, 0);
+      float sy = p.up_h > 1 ? (float)(p.H - 1) / (float)(p.up_h - 1) : 0.f;
+      float sx = p.up_w > 1 ? (float)(p.W - 1) / (float)(p.up_w - 1) : 0.f;
+      float fy = sy * iy, fx = sx * ix;
+      int y0 = (int)fy, x0 = (int)fx;
+      int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
+      float wy = fy - y0, wx = fx - x0;
+      const h16* base = p.x + (long)bt[i] * p.H * p.W * p.Cin + ci;
+      h8 a = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * p.W + x0) * p.Cin));
+      h8 b = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * p.W + x1) * p.Cin));
+      h8 c = __builtin_bit_cast(h8, ldg16(base + ((long)y1 * p.W + x0) * p.Cin));
+      h8 d = __builtin_bit_cast(h8, ldg16(base + ((long)y1 * p.W + x1) * p.Cin));
+      h8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float top = (float)a[j] + ((float)b[j] - (float)a[j]) * wx;
+        float bot = (float)c[j] + ((float)d[j] - (float)c[j]) * wx;
+        o[j] = (h16)(top + (bot - top) * wy);
+      }
+      v = __builtin_bit_cast(uint4, o);
+    } else {
+      if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) return make_uint4(0, 0, 0, 0);
+      v = ldg16(p.x + (((long)bt[i] * p.H + iy) * p.W + ix) * p.Cin + ci);
+    }
+    if (p.pre_relu) v = relu_h8(v);
+    return v;
+  }
+};
+
+// ---- epilogue ------------------------------------------------------------------------------
+__device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4 v) {
+  const vda_epilogue& e = p.epi;
+  if (e.bias) {
+    f4 b = *reinterpret_cast<const f4*>(e.bias + n);
+    v += b;
+  }
+  if (e.rowbias) {
+    int r = (m / e.rdiv) % e.rmod;
+    f4 b = *reinterpret_cast<const f4*>(e.rowbias + (long)r * p.N + n);
+    v += b;
+  }
+  if (e.act == VDA_ACT_GELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
+  } else if (e.act == VDA_ACT_RELU) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
+  }
+  if (e.gamma) {
+    f4 g = *reinterpret_cast<const f4*>(e.gamma + n);
+    v *= g;
+  }
+  if (e.res) {
+    h4 r = *reinterpret_cast<const h4*>((const h16*)e.res + (long)m * e.ldres + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+  }
+  if (e.res2) {
+    h4 r = *reinterpret_cast<const h4*>((const h16*)e.res2 + (long)m * e.ldres2 + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+  }
+  h4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (h16)v[j];
+  long off;
+  if (e.store == VDA_STORE_PIXEL_SHUFFLE) {
+    int k = e.ps_k, cout = e.ps_cout;
+    int ij = n / cout, co = n - ij * cout;
+    int ki = ij / k, kj = ij - ki * k;
+    int xw = m % e.ps_win;
+    int t = m / e.ps_win;
+    int yh = t % e.ps_hin;
+    int bt = t / e.ps_hin;
+    long oh = (long)yh * k + ki, ow = (long)xw * k + kj;
+    off = (((long)bt * e.ps_hin * k + oh) * ((long)e.ps_win * k) + ow) * cout + co;
+  } else {
+    off = (long)m * p.ldy + n;
+  }
+  *reinterpret_cast<h4*>(p.y + off) = o;
+}
+
+// GEGLU: h and g accumulators for the same 4 output channels.  Output column = n_out.
+__device__ __forceinline__ void epi_geglu4(const GemmParams& p, int m, int nh, int ng, int n_out,
+                                           f4 vh, f4 vg) {
+  const vda_epilogue& e = p.epi;
+  if (e.bias) {
+    vh += *reinterpret_cast<const f4*>(e.bias + nh);
+    vg += *reinterpret_cast<const f4*>(e.bias + ng);
+  }
+  f4 v;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = vh[j] * gelu_erf(vg[j]);
+  const int nout_tot = p.N >> 1;
+  if (e.gamma) v *= *reinterpret_cast<const f4*>(e.gamma + n_out);
+  if (e.res) {
+    h4 r = *reinterpret_cast<const h4*>((const h16*)e.res + (long)m * e.ldres + n_out);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] += (float)r[j];
+  }
+  (void)nout_tot;
+  h4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = (h16)v[j];
+  *reinterpret_cast<h4*>(p.y + (long)m * p.ldy + n_out) = o;
+}
+
+// ---- main kernel ---------------------------------------------------------------------------
+template <int BM, int BN, class Loader>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
+  constexpr int TM = BM / 32;  // 16-row m subtiles per wave
+  constexpr int TN = BN / 32;  // 16-row n subtiles per wave
+  constexpr int XIT = BM / 32; // 16-B chunks per thread for the X tile (BM*8 / 256)
+  constexpr int WIT = BN / 32;
+  __shared__ __attribute__((aligned(16))) h16 sX[2][BM * BK];
+  __shared__ __attribute__((aligned(16))) h16 sW[2][BN * BK];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int tile_n = blockIdx.x % tiles_n, tile_m = blockIdx.x / tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  Loader ld;
+  ld.init(p, m0, tid, XIT);
+  const h16* wrow[WIT];
+  bool wok[WIT];
+#pragma unroll
+  for (int i = 0; i < WIT; ++i) {
+    int n = n0 + (tid >> 3) + 32 * i;
+    wok[i] = n < p.N;
+    wrow[i] = p.w + (long)(wok[i] ? n : 0) * p.K;
+  }
+  const int cchunk = tid & 7;
+
+  uint4 rx[XIT], rw[WIT];
+  auto gload = [&](int k0) {
+    int k = k0 + cchunk * 8;
+#pragma unroll
+    for (int i = 0; i < XIT; ++i) rx[i] = ld.load(p, i, k);
+#pragma unroll
+    for (int i = 0; i < WIT; ++i) rw[i] = (wok[i] && k < p.K) ? ldg16(wrow[i] + k) : make_uint4(0, 0, 0, 0);
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XIT; ++i) *reinterpret_cast<uint4*>(&sX[buf][swz((tid >> 3) + 32 * i, cchunk)]) = rx[i];
+#pragma unroll
+    for (int i = 0; i < WIT; ++i) *reinterpret_cast<uint4*>(&sW[buf][swz((tid >> 3) + 32 * i, cchunk)]) = rw[i];
+  };
+
+  f4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+
+  const int frow = lane & 15, fchunk = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 af[TN], bf[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *reinterpret_cast<const h8*>(&sW[buf][swz(wn * (BN / 2) + i * 16 + frow, ks * 4 + fchunk)]);
+#pragma unroll
+      for (int j = 0; j < TM; ++j)
+        bf[j] = *reinterpret_cast<const h8*>(&sX[buf][swz(wm * (BM / 2) + j * 16 + frow, ks * 4 + fchunk)]);
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds D[n = 4*(lane>>4) + r][m = lane&15] of every (i, j) subtile
+  const int mcol = lane & 15, nq = (lane >> 4) * 4;
+  if (p.epi.act == VDA_ACT_GEGLU) {
+#pragma unroll
+    for (int i = 0; i < TN; i += 2) {
+      const int nbase = n0 + wn * (BN / 2) + i * 16;  // h block; gate block = nbase + 16
+      if (nbase >= p.N) continue;
+      const int n_out = (nbase >> 1) + nq;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        int m = m0 + wm * (BM / 2) + j * 16 + mcol;
+        if (m < p.M) epi_geglu4(p, m, nbase + nq, nbase + 16 + nq, n_out, acc[i][j], acc[i + 1][j]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * (BN / 2) + i * 16 + nq;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        int m = m0 + wm * (BM / 2) + j * 16 + mcol;
+        if (m < p.M) epi_store4(p, m, n, acc[i][j]);
+      }
+    }
+  }
+}
+
+template <class Loader>
+int launch(const GemmParams& p, hipStream_t st) {
+  // tile choice: wide tiles for big N, narrow for the DPT head's small channel counts
+  int tiles_m, tiles_n;
+  if (p.N >= 128) {
+    tiles_m = (p.M + 127) / 128; tiles_n = (p.N + 127) / 128;
+    hipLaunchKernelGGL((gemm_kernel<128, 128, Loader>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  } else {
+    tiles_m = (p.M + 127) / 128; tiles_n = (p.N + 63) / 64;
+    hipLaunchKernelGGL((gemm_kernel<128, 64, Loader>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  }
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+vda_epilogue default_epi() {
+  vda_epilogue e{};
+  e.rdiv = 1; e.rmod = 1;
+  return e;
+}
+
+int check_epi(const vda_epilogue& e, int N) {
+  VDA_CHECK_ARG(!e.rowbias || (e.rdiv > 0 && e.rmod > 0), "rowbias needs rdiv, rmod > 0");
+  VDA_CHECK_ARG(e.act >= 0 && e.act <= 3, "unknown activation");
+  VDA_CHECK_ARG(e.act != VDA_ACT_GEGLU || (N % 32 == 0 && !e.rowbias && e.store == 0 && !e.res2),
+                "GEGLU needs N % 32 == 0, no rowbias/res2, row store");
+  VDA_CHECK_ARG(e.store == VDA_STORE_ROWS ||
+                (e.store == VDA_STORE_PIXEL_SHUFFLE && e.ps_k > 0 && e.ps_cout > 0 && e.ps_cout % 4 == 0 &&
+                 e.ps_hin > 0 && e.ps_win > 0 && N == e.ps_k * e.ps_k * e.ps_cout && !e.res && !e.res2),
+                "bad pixel-shuffle store geometry");
+  VDA_CHECK_ARG(!e.res || e.ldres % 4 == 0, "ldres % 4");
+  VDA_CHECK_ARG(!e.res2 || e.ldres2 % 4 == 0, "ldres2 % 4");
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy, int32_t M,
+                        int32_t N, int32_t K, const vda_epilogue* epi, void* stream) {
+  VDA_CHECK_ARG(x && w && y, "null pointer");
+  VDA_CHECK_ARG(M > 0 && N > 0 && K > 0, "empty GEMM");
+  VDA_CHECK_ARG(K % 8 == 0 && ldx % 8 == 0 && ldx >= K, "K and ldx must be multiples of 8, ldx >= K");
+  VDA_CHECK_ARG(N % 4 == 0 && ldy % 4 == 0, "N and ldy must be multiples of 4");
+  GemmParams p{};
+  p.x = (const h16*)x; p.ldx = ldx; p.w = (const h16*)w; p.y = (h16*)y; p.ldy = ldy;
+  p.M = M; p.N = N; p.K = K;
+  p.epi = epi ? *epi : default_epi();
+  if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
+  if (p.epi.rmod <= 0) p.epi.rmod = 1;
+  int rc = check_epi(p.epi, N);
+  if (rc) return rc;
+  return launch<DenseLoader>(p, (hipStream_t)stream);
+}
+
+extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
+                          int32_t Cin, int32_t Cout, int32_t ks, int32_t stride, int32_t pad,
+                          int32_t pre_relu, int32_t up_h, int32_t up_w, const vda_epilogue* epi,
+                          void* stream) {
+  VDA_CHECK_ARG(x && w && y, "null pointer");
+  VDA_CHECK_ARG(BT > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && ks > 0 && stride > 0 && pad >= 0,
+                "bad conv geometry");
+  VDA_CHECK_ARG(Cin % 8 == 0 && Cout % 4 == 0, "Cin % 8 and Cout % 4 required");
+  const int Hi = up_h > 0 ? up_h : H, Wi = up_w > 0 ? up_w : W;
+  GemmParams p{};
+  p.x = (const h16*)x; p.w = (const h16*)w; p.y = (h16*)y;
+  p.H = H; p.W = W; p.Cin = Cin; p.ks = ks; p.stride = stride; p.pad = pad; p.pre_relu = pre_relu;
+  p.up_h = up_h > 0 ? up_h : 0; p.up_w = up_w > 0 ? up_w : 0;
+  p.Ho = (Hi + 2 * pad - ks) / stride + 1;
+  p.Wo = (Wi + 2 * pad - ks) / stride + 1;
+  VDA_CHECK_ARG(p.Ho > 0 && p.Wo > 0, "empty conv output");
+  p.M = BT * p.Ho * p.Wo; p.N = Cout; p.K = ks * ks * Cin;
+  p.ldy = Cout; p.ldx = 0;
+  p.epi = epi ? *epi : default_epi();
+  if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
+  if (p.epi.rmod <= 0) p.epi.rmod = 1;
+  VDA_CHECK_ARG(p.epi.store == VDA_STORE_ROWS && p.epi.act != VDA_ACT_GEGLU, "conv: row store, no GEGLU");
+  int rc = check_epi(p.epi, Cout);
+  if (rc) return rc;
+  return launch<ConvLoader>(p, (hipStream_t)stream);
+}

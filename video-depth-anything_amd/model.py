@@ -1,0 +1,502 @@
+"""VideoDepthAnything for MI355X: the reference module API and state_dict schema, HIP forward.
+
+The module tree mirrors the reference's attribute names exactly
+(video_depth.py:35-56, dinov2.py:44-170, dinov2_layers/*, dpt.py:47-124, dpt_temporal.py:23-51,
+motion_module/*, util/blocks.py), so a reference checkpoint loads with ``strict=True``.  The
+tree only *holds* parameters: ``forward`` never calls the sub-modules.  On first use on a device
+the parameters are packed once into kernel-ready form (fp16 K-contiguous weights, fp32 biases,
+NHWC conv weights, pixel-shuffle ConvT weights, GEGLU row interleave, the temporal
+positional-encoding folded through to_q/k/v as a per-frame bias) and the whole clip forward then
+runs on libvda kernels with NHWC / token-major activations.
+
+``forward(x[B, T, 3, H, W] float, skip_tmp_block=False) -> depth[B, T, H, W] float`` matches
+``VideoDepthAnything.forward`` (video_depth.py:58-65).  Inference only; fp16 compute with fp32
+accumulation, statistics and depth tail (dpt_temporal.py:95-97 keeps output_conv2 in fp32).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from ._lib import ACT_GELU, ACT_GEGLU, ACT_RELU
+
+PATCH = 14
+ENCODER_CFG = {
+    "vits": dict(embed_dim=384, depth=12, heads=6, taps=[2, 5, 8, 11]),
+    "vitb": dict(embed_dim=768, depth=12, heads=12, taps=[2, 5, 8, 11]),
+    "vitl": dict(embed_dim=1024, depth=24, heads=16, taps=[4, 11, 17, 23]),
+}
+# run.py:74-77 model_configs
+MODEL_CONFIGS = {
+    "vits": dict(encoder="vits", features=64, out_channels=[48, 96, 192, 384]),
+    "vitb": dict(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
+    "vitl": dict(encoder="vitl", features=256, out_channels=[256, 512, 1024, 1024]),
+}
+
+
+# ---------------------------------------------------------------------------------------------
+# Parameter-holding module tree (names == reference state_dict keys)
+# ---------------------------------------------------------------------------------------------
+class LayerScale(nn.Module):  # layer_scale.py:16-28
+    def __init__(self, dim):
+        super().__init__()
+        self.gamma = nn.Parameter(torch.ones(dim))
+
+
+class Attention(nn.Module):  # dinov2_layers/attention.py:29-47
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.num_heads = heads
+        self.qkv = nn.Linear(dim, 3 * dim, bias=True)
+        self.proj = nn.Linear(dim, dim, bias=True)
+
+
+class Mlp(nn.Module):  # mlp.py:17-33
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class Block(nn.Module):  # block.py:36-80
+    def __init__(self, dim, heads):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.ls1 = LayerScale(dim)
+        self.norm2 = nn.LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, 4 * dim)
+        self.ls2 = LayerScale(dim)
+
+
+class PatchEmbed(nn.Module):  # patch_embed.py:26-67
+    def __init__(self, dim):
+        super().__init__()
+        self.proj = nn.Conv2d(3, dim, kernel_size=PATCH, stride=PATCH)
+
+
+class DinoVisionTransformer(nn.Module):  # dinov2.py:44-170, DINOv2() factory :398-415
+    def __init__(self, encoder):
+        super().__init__()
+        cfg = ENCODER_CFG[encoder]
+        C = cfg["embed_dim"]
+        self.embed_dim = C
+        self.num_heads = cfg["heads"]
+        self.patch_size = PATCH
+        self.patch_embed = PatchEmbed(C)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, C))
+        self.pos_embed = nn.Parameter(torch.zeros(1, (518 // PATCH) ** 2 + 1, C))
+        self.blocks = nn.ModuleList([Block(C, cfg["heads"]) for _ in range(cfg["depth"])])
+        self.norm = nn.LayerNorm(C, eps=1e-6)
+        self.mask_token = nn.Parameter(torch.zeros(1, C))
+
+
+class ResidualConvUnit(nn.Module):  # blocks.py:37-66
+    def __init__(self, f):
+        super().__init__()
+        self.conv1 = nn.Conv2d(f, f, 3, 1, 1, bias=True)
+        self.conv2 = nn.Conv2d(f, f, 3, 1, 1, bias=True)
+
+
+class FeatureFusionBlock(nn.Module):  # blocks.py:94-133
+    def __init__(self, f):
+        super().__init__()
+        self.out_conv = nn.Conv2d(f, f, 1, 1, 0, bias=True)
+        self.resConfUnit1 = ResidualConvUnit(f)
+        self.resConfUnit2 = ResidualConvUnit(f)
+
+
+class PositionalEncoding(nn.Module):  # motion_module.py:189-207
+    def __init__(self, d_model, max_len=32):
+        super().__init__()
+        pos = torch.arange(max_len).unsqueeze(1)
+        div = torch.exp(torch.arange(0, d_model, 2) * (-math.log(10000.0) / d_model))
+        pe = torch.zeros(1, max_len, d_model)
+        pe[0, :, 0::2] = torch.sin(pos * div)
+        pe[0, :, 1::2] = torch.cos(pos * div)
+        self.register_buffer("pe", pe)
+
+
+class TemporalAttention(nn.Module):  # motion_module.py:210-245 over attention.py:30-92
+    def __init__(self, dim, max_len):
+        super().__init__()
+        self.heads = 8
+        self.to_q = nn.Linear(dim, dim, bias=False)
+        self.to_k = nn.Linear(dim, dim, bias=False)
+        self.to_v = nn.Linear(dim, dim, bias=False)
+        self.to_out = nn.ModuleList([nn.Linear(dim, dim), nn.Dropout(0.0)])
+        self.pos_encoder = PositionalEncoding(dim, max_len)
+
+
+class GEGLU(nn.Module):  # attention.py:363-384
+    def __init__(self, dim, inner):
+        super().__init__()
+        self.proj = nn.Linear(dim, 2 * inner)
+
+
+class FeedForward(nn.Module):  # attention.py:296-338
+    def __init__(self, dim):
+        super().__init__()
+        self.net = nn.ModuleList([GEGLU(dim, 4 * dim), nn.Dropout(0.0), nn.Linear(4 * dim, dim)])
+
+
+class TemporalTransformerBlock(nn.Module):  # motion_module.py:136-170
+    def __init__(self, dim, max_len):
+        super().__init__()
+        self.attention_blocks = nn.ModuleList([TemporalAttention(dim, max_len) for _ in range(2)])
+        self.norms = nn.ModuleList([nn.LayerNorm(dim) for _ in range(2)])
+        self.ff = FeedForward(dim)
+        self.ff_norm = nn.LayerNorm(dim)
+
+
+class TemporalTransformer3DModel(nn.Module):  # motion_module.py:72-106
+    def __init__(self, C, max_len):
+        super().__init__()
+        self.norm = nn.GroupNorm(32, C, eps=1e-6, affine=True)
+        self.proj_in = nn.Linear(C, C)
+        self.transformer_blocks = nn.ModuleList([TemporalTransformerBlock(C, max_len)])
+        self.proj_out = nn.Linear(C, C)
+
+
+class TemporalModule(nn.Module):  # motion_module.py:32-69 (num_transformer_block=1, dpt_temporal.py:35-40)
+    def __init__(self, C, max_len=32):
+        super().__init__()
+        self.temporal_transformer = TemporalTransformer3DModel(C, max_len)
+
+
+class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
+    def __init__(self, in_channels, features, out_channels, num_frames=32):
+        super().__init__()
+        self.projects = nn.ModuleList([nn.Conv2d(in_channels, oc, 1) for oc in out_channels])
+        self.resize_layers = nn.ModuleList([
+            nn.ConvTranspose2d(out_channels[0], out_channels[0], 4, 4, 0),
+            nn.ConvTranspose2d(out_channels[1], out_channels[1], 2, 2, 0),
+            nn.Identity(),
+            nn.Conv2d(out_channels[3], out_channels[3], 3, 2, 1),
+        ])
+        s = nn.Module()
+        s.layer1_rn = nn.Conv2d(out_channels[0], features, 3, 1, 1, bias=False)
+        s.layer2_rn = nn.Conv2d(out_channels[1], features, 3, 1, 1, bias=False)
+        s.layer3_rn = nn.Conv2d(out_channels[2], features, 3, 1, 1, bias=False)
+        s.layer4_rn = nn.Conv2d(out_channels[3], features, 3, 1, 1, bias=False)
+        s.refinenet1 = FeatureFusionBlock(features)
+        s.refinenet2 = FeatureFusionBlock(features)
+        s.refinenet3 = FeatureFusionBlock(features)
+        s.refinenet4 = FeatureFusionBlock(features)
+        s.output_conv1 = nn.Conv2d(features, features // 2, 3, 1, 1)
+        s.output_conv2 = nn.Sequential(nn.Conv2d(features // 2, 32, 3, 1, 1), nn.ReLU(True),
+                                       nn.Conv2d(32, 1, 1, 1, 0), nn.ReLU(True), nn.Identity())
+        self.scratch = s
+        self.motion_modules = nn.ModuleList([
+            TemporalModule(out_channels[2], num_frames), TemporalModule(out_channels[3], num_frames),
+            TemporalModule(features, num_frames), TemporalModule(features, num_frames)])
+
+
+# ---------------------------------------------------------------------------------------------
+# Packed (kernel-ready) weights
+# ---------------------------------------------------------------------------------------------
+def _h(t):
+    return t.detach().to(torch.float16).contiguous()
+
+
+def _f(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+def _conv_nhwc(w):  # [Cout, Cin, kh, kw] -> [Cout, kh, kw, Cin] fp16
+    return _h(w.detach().permute(0, 2, 3, 1))
+
+
+def _geglu_interleave(t):
+    """Rows [h(0..I-1); g(0..I-1)] -> 16-row blocks [h(16p..16p+15); g(16p..16p+15)] (vda.h GEGLU)."""
+    inner = t.shape[0] // 2
+    hh, gg = t[:inner], t[inner:]
+    blocks = []
+    for p in range(0, inner, 16):
+        blocks += [hh[p:p + 16], gg[p:p + 16]]
+    return torch.cat(blocks, 0)
+
+
+class _Packed:
+    pass
+
+
+class VideoDepthAnything(nn.Module):
+    """Reference-compatible constructor (video_depth.py:36-45) and forward (:58-65)."""
+
+    def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
+                 use_clstoken=False, num_frames=32, pe="ape"):
+        super().__init__()
+        if use_bn or use_clstoken or pe != "ape":
+            raise NotImplementedError("only the shipped configuration (use_bn=False, use_clstoken=False, "
+                                      "pe='ape') is on the accelerated path")
+        self.intermediate_layer_idx = {k: v["taps"] for k, v in ENCODER_CFG.items()}
+        self.encoder = encoder
+        self.num_frames = num_frames
+        self.features = features
+        self.out_channels = list(out_channels)
+        self.pretrained = DinoVisionTransformer(encoder)
+        self.head = DPTHeadTemporal(self.pretrained.embed_dim, features, self.out_channels, num_frames)
+        self._packed: Dict[str, _Packed] = {}
+        self._pos_cache: Dict[tuple, torch.Tensor] = {}
+
+    @classmethod
+    def from_config(cls, encoder: str, device="meta"):
+        """Build without running torch's default initialisers (weights are loaded afterwards)."""
+        with torch.device(device):
+            m = cls(**MODEL_CONFIGS[encoder])
+        return m
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        self._packed.clear()
+        self._pos_cache.clear()
+        return super().load_state_dict(state_dict, strict=strict, assign=assign)
+
+    # -- packing ---------------------------------------------------------------------------
+    @torch.no_grad()
+    def _pack(self, device) -> _Packed:
+        key = str(device)
+        if key in self._packed:
+            return self._packed[key]
+        dev = torch.device(device)
+        P = _Packed()
+        enc = self.pretrained
+        C = enc.embed_dim
+        P.C, P.heads = C, enc.num_heads
+        P.Kp = 592  # 588 = 3*14*14 rounded up to a multiple of 8
+        wpe = enc.patch_embed.proj.weight.reshape(C, -1)
+        P.patch_w = _h(F.pad(wpe, (0, P.Kp - wpe.shape[1]))).to(dev)
+        P.patch_b = _f(enc.patch_embed.proj.bias).to(dev)
+        P.cls = _f(enc.cls_token.reshape(C)).to(dev)
+        P.pos = _f(enc.pos_embed).to(dev)
+        P.blocks = []
+        for b in enc.blocks:
+            q = _Packed()
+            q.n1w, q.n1b = _f(b.norm1.weight).to(dev), _f(b.norm1.bias).to(dev)
+            q.qkv_w, q.qkv_b = _h(b.attn.qkv.weight).to(dev), _f(b.attn.qkv.bias).to(dev)
+            q.proj_w, q.proj_b = _h(b.attn.proj.weight).to(dev), _f(b.attn.proj.bias).to(dev)
+            q.ls1 = _f(b.ls1.gamma).to(dev)
+            q.n2w, q.n2b = _f(b.norm2.weight).to(dev), _f(b.norm2.bias).to(dev)
+            q.fc1_w, q.fc1_b = _h(b.mlp.fc1.weight).to(dev), _f(b.mlp.fc1.bias).to(dev)
+            q.fc2_w, q.fc2_b = _h(b.mlp.fc2.weight).to(dev), _f(b.mlp.fc2.bias).to(dev)
+            q.ls2 = _f(b.ls2.gamma).to(dev)
+            P.blocks.append(q)
+        P.nw, P.nb = _f(enc.norm.weight).to(dev), _f(enc.norm.bias).to(dev)
+
+        hd = self.head
+        P.proj_w = [_h(c.weight.reshape(c.weight.shape[0], -1)).to(dev) for c in hd.projects]
+        P.proj_b = [_f(c.bias).to(dev) for c in hd.projects]
+        P.rs_w, P.rs_b = {}, {}
+        for i, k in ((0, 4), (1, 2)):
+            ct = hd.resize_layers[i]
+            w = ct.weight  # [Cin, Cout, k, k] -> rows (i, j, co), K = Cin
+            P.rs_w[i] = _h(w.permute(2, 3, 1, 0).reshape(k * k * w.shape[1], w.shape[0])).to(dev)
+            P.rs_b[i] = _f(ct.bias.repeat(k * k)).to(dev)
+        P.rs_w[3] = _conv_nhwc(hd.resize_layers[3].weight).to(dev)
+        P.rs_b[3] = _f(hd.resize_layers[3].bias).to(dev)
+        s = hd.scratch
+        P.rn = [_conv_nhwc(getattr(s, f"layer{i}_rn").weight).to(dev) for i in range(1, 5)]
+        P.ref = {}
+        for i in range(1, 5):
+            r = getattr(s, f"refinenet{i}")
+            q = _Packed()
+            q.out_w, q.out_b = _h(r.out_conv.weight.reshape(r.out_conv.weight.shape[0], -1)).to(dev), _f(r.out_conv.bias).to(dev)
+            for u in (1, 2):
+                rcu = getattr(r, f"resConfUnit{u}")
+                setattr(q, f"r{u}c1_w", _conv_nhwc(rcu.conv1.weight).to(dev))
+                setattr(q, f"r{u}c1_b", _f(rcu.conv1.bias).to(dev))
+                setattr(q, f"r{u}c2_w", _conv_nhwc(rcu.conv2.weight).to(dev))
+                setattr(q, f"r{u}c2_b", _f(rcu.conv2.bias).to(dev))
+            P.ref[i] = q
+        P.oc1_w, P.oc1_b = _conv_nhwc(s.output_conv1.weight).to(dev), _f(s.output_conv1.bias).to(dev)
+        oc2 = s.output_conv2
+        P.oc2_w1 = _f(oc2[0].weight.permute(0, 2, 3, 1)).to(dev)  # [32, 3, 3, C] fp32
+        P.oc2_b1 = _f(oc2[0].bias).to(dev)
+        P.oc2_w2 = _f(oc2[2].weight.reshape(-1)).to(dev)
+        P.oc2_b2 = _f(oc2[2].bias).to(dev)
+
+        P.mm = []
+        for m in hd.motion_modules:
+            tt = m.temporal_transformer
+            q = _Packed()
+            Cm = tt.proj_in.weight.shape[0]
+            q.C = Cm
+            q.gnw, q.gnb = _f(tt.norm.weight).to(dev), _f(tt.norm.bias).to(dev)
+            q.pin_w, q.pin_b = _h(tt.proj_in.weight).to(dev), _f(tt.proj_in.bias).to(dev)
+            q.pout_w, q.pout_b = _h(tt.proj_out.weight).to(dev), _f(tt.proj_out.bias).to(dev)
+            blk = tt.transformer_blocks[0]
+            q.attn = []
+            for ab, nrm in zip(blk.attention_blocks, blk.norms):
+                a = _Packed()
+                a.nw, a.nb = _f(nrm.weight).to(dev), _f(nrm.bias).to(dev)
+                wqkv = torch.cat([ab.to_q.weight, ab.to_k.weight, ab.to_v.weight], 0).float()
+                a.qkv_w = _h(wqkv).to(dev)
+                # (n + pe[t]) Wᵀ = n Wᵀ + pe[t] Wᵀ: the PE add (motion_module.py:255-256) becomes a
+                # per-frame fp32 row bias of the fused q/k/v GEMM.
+                a.pe_bias = _f(ab.pos_encoder.pe[0].float() @ wqkv.t()).to(dev)  # [max_len, 3C]
+                a.out_w, a.out_b = _h(ab.to_out[0].weight).to(dev), _f(ab.to_out[0].bias).to(dev)
+                q.attn.append(a)
+            q.ffnw, q.ffnb = _f(blk.ff_norm.weight).to(dev), _f(blk.ff_norm.bias).to(dev)
+            q.ff1_w = _h(_geglu_interleave(blk.ff.net[0].proj.weight)).to(dev)
+            q.ff1_b = _f(_geglu_interleave(blk.ff.net[0].proj.bias)).to(dev)
+            q.ff2_w, q.ff2_b = _h(blk.ff.net[2].weight).to(dev), _f(blk.ff.net[2].bias).to(dev)
+            P.mm.append(q)
+        self._packed[key] = P
+        return P
+
+    def _token_bias(self, P: _Packed, H: int, W: int, device) -> torch.Tensor:
+        """Per-token fp32 bias [1+np, C]: cls+pos[0] for the cls row, conv bias + pos for patches.
+        The bicubic resize of the pos table (dinov2.py:179-210) runs once per resolution (glue)."""
+        key = (H, W, str(device))
+        if key in self._pos_cache:
+            return self._pos_cache[key]
+        pos = P.pos  # [1, 1+N0, C]
+        N0 = pos.shape[1] - 1
+        ph, pw = H // PATCH, W // PATCH
+        if ph * pw == N0 and H == W:
+            pe = pos[0]
+        else:
+            s0 = math.sqrt(N0)
+            C = pos.shape[-1]
+            pp = pos[:, 1:].reshape(1, int(s0), int(s0), C).permute(0, 3, 1, 2)
+            pp = F.interpolate(pp, scale_factor=((ph + 0.1) / s0, (pw + 0.1) / s0), mode="bicubic",
+                               antialias=False)
+            assert pp.shape[-2:] == (ph, pw)
+            pe = torch.cat([pos[0, :1], pp.permute(0, 2, 3, 1).reshape(ph * pw, C)], 0)
+        tb = pe.clone()
+        tb[0] += P.cls
+        tb[1:] += P.patch_b
+        tb = tb.contiguous()
+        self._pos_cache[key] = tb
+        return tb
+
+    # -- forward ---------------------------------------------------------------------------
+    def _temporal(self, q: _Packed, x: torch.Tensor, B: int, T: int, S: int) -> torch.Tensor:
+        """TemporalModule on token-major frames x [B*T*S, C] (motion_module.py:64-133)."""
+        C = q.C
+        xn = ops.groupnorm(x, q.gnw, q.gnb, B * T, 32, 1e-6)
+        h = ops.gemm(xn, q.pin_w, bias=q.pin_b)
+        for a in q.attn:
+            n = ops.layernorm(h, a.nw, a.nb, 1e-5)
+            qkv = ops.gemm(n, a.qkv_w, rowbias=a.pe_bias, rdiv=S, rmod=T)
+            at = ops.temporal_attention(qkv, B, T, S, 8, C // 8)
+            h = ops.gemm(at, a.out_w, bias=a.out_b, res=h, out=h)
+        n = ops.layernorm(h, q.ffnw, q.ffnb, 1e-5)
+        g = ops.gemm(n, q.ff1_w, bias=q.ff1_b, act=ACT_GEGLU)
+        h = ops.gemm(g, q.ff2_w, bias=q.ff2_b, res=h, out=h)
+        return ops.gemm(h, q.pout_w, bias=q.pout_b, res=x)
+
+    def _fusion(self, q: _Packed, x0, x1, size):
+        """FeatureFusionBlock (blocks.py:135-162) on NHWC maps; the 1x1 out_conv commutes with the
+        bilinear resize (both linear, resize weights sum to 1), so it runs at the low resolution."""
+        if x1 is not None:
+            t = ops.conv2d(x1, q.r1c1_w, bias=q.r1c1_b, pre_relu=True, act=ACT_RELU)
+            out = ops.conv2d(t, q.r1c2_w, bias=q.r1c2_b, res=x1, res2=x0)
+        else:
+            out = x0
+        t = ops.conv2d(out, q.r2c1_w, bias=q.r2c1_b, pre_relu=True, act=ACT_RELU)
+        out = ops.conv2d(t, q.r2c2_w, bias=q.r2c2_b, res=out)
+        BT, h, w, Cf = out.shape
+        y = ops.gemm(out.view(-1, Cf), q.out_w, bias=q.out_b).view(BT, h, w, Cf)
+        return y, size
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, skip_tmp_block: bool = False) -> torch.Tensor:
+        if not x.is_cuda:
+            raise RuntimeError("VideoDepthAnything (MI355X) runs on the GPU only; move the model input to cuda")
+        B, T, Cc, H, W = x.shape
+        if Cc != 3:
+            raise ValueError(f"expected 3 input channels, got {Cc}")
+        if H % PATCH or W % PATCH:  # patch_embed.py:73-74
+            raise AssertionError(f"Input image size ({H}x{W}) is not a multiple of the patch size {PATCH}")
+        if T > self.num_frames:  # PE table length (motion_module.py:198-206)
+            raise ValueError(f"clip length {T} exceeds the temporal PE table ({self.num_frames})")
+        dev = x.device
+        P = self._pack(dev)
+        BT = B * T
+        ph, pw = H // PATCH, W // PATCH
+        npt = ph * pw
+        ntok = npt + 1
+        C = P.C
+
+        # ---- DINOv2 encoder (dinov2.py:212-231, :271-321; block.py:104-106)
+        img = x.reshape(BT, 3, H, W).float().contiguous()
+        a = ops.patch_im2col(img, P.Kp)
+        tok = ops.gemm(a, P.patch_w, rowbias=self._token_bias(P, H, W, dev), rdiv=1, rmod=ntok)
+        del a
+        taps = self.intermediate_layer_idx[self.encoder]
+        feats: List[torch.Tensor] = []
+        for i, q in enumerate(P.blocks):
+            hN = ops.layernorm(tok, q.n1w, q.n1b, 1e-6)
+            qkv = ops.gemm(hN, q.qkv_w, bias=q.qkv_b)
+            at = ops.spatial_attention(qkv, BT, ntok, P.heads, 64)
+            del qkv
+            ops.gemm(at, q.proj_w, bias=q.proj_b, gamma=q.ls1, res=tok, out=tok)
+            hN = ops.layernorm(tok, q.n2w, q.n2b, 1e-6)
+            f = ops.gemm(hN, q.fc1_w, bias=q.fc1_b, act=ACT_GELU)
+            ops.gemm(f, q.fc2_w, bias=q.fc2_b, gamma=q.ls2, res=tok, out=tok)
+            del f
+            if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
+                feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
+        del tok
+
+        # ---- DPT reassemble (dpt_temporal.py:55-69, dpt.py:60-90)
+        oc = self.out_channels
+        lay = []
+        for i, ft in enumerate(feats):
+            p = ops.gemm(ft, P.proj_w[i], bias=P.proj_b[i])
+            if i == 0:
+                l = ops.conv_transpose_ks(p, P.rs_w[0], P.rs_b[0], BT, ph, pw, 4)
+            elif i == 1:
+                l = ops.conv_transpose_ks(p, P.rs_w[1], P.rs_b[1], BT, ph, pw, 2)
+            elif i == 2:
+                l = p.view(BT, ph, pw, oc[2])
+            else:
+                l = ops.conv2d(p.view(BT, ph, pw, oc[3]), P.rs_w[3], ks=3, stride=2, pad=1, bias=P.rs_b[3])
+            lay.append(l)
+        del feats
+        l1, l2, l3, l4 = lay
+        h3, w3 = l3.shape[1:3]
+        h4, w4 = l4.shape[1:3]
+        # temporal modules on layer_3 / layer_4 (dpt_temporal.py:75-76)
+        l3 = self._temporal(P.mm[0], l3.reshape(-1, oc[2]), B, T, h3 * w3).view(BT, h3, w3, oc[2])
+        l4 = self._temporal(P.mm[1], l4.reshape(-1, oc[3]), B, T, h4 * w4).view(BT, h4, w4, oc[3])
+        r1 = ops.conv2d(l1, P.rn[0])
+        r2 = ops.conv2d(l2, P.rn[1])
+        r3 = ops.conv2d(l3, P.rn[2])
+        r4 = ops.conv2d(l4, P.rn[3])
+        del l1, l2, l3, l4, lay
+        Fh = self.features
+        y, _ = self._fusion(P.ref[4], r4, None, None)
+        p4 = ops.upsample_bilinear(y, r3.shape[1], r3.shape[2])
+        if not skip_tmp_block:
+            p4 = self._temporal(P.mm[2], p4.view(-1, Fh), B, T, h3 * w3).view(p4.shape)
+        y, _ = self._fusion(P.ref[3], p4, r3, None)
+        p3 = ops.upsample_bilinear(y, r2.shape[1], r2.shape[2])
+        p3 = self._temporal(P.mm[3], p3.view(-1, Fh), B, T, p3.shape[1] * p3.shape[2]).view(p3.shape)
+        y, _ = self._fusion(P.ref[2], p3, r2, None)
+        p2 = ops.upsample_bilinear(y, r1.shape[1], r1.shape[2])
+        y, _ = self._fusion(P.ref[1], p2, r1, None)  # refinenet1: scale_factor 2
+        H1, W1 = 2 * y.shape[1], 2 * y.shape[2]
+        # output_conv1 on the x2 bilinear upsample, read through the conv's loader (no 296² tensor)
+        o1 = ops.conv2d(y, P.oc1_w, bias=P.oc1_b, up=(H1, W1))
+        # output_conv2 in fp32 on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
+        # the final resize to (H, W) is the identity because H = 14ph, W = 14pw (video_depth.py:63)
+        depth = ops.depth_head(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
+        return depth.view(B, T, H, W)
+
+
+def build_model(encoder: str = "vitl", state_dict: Optional[dict] = None, device="cuda") -> VideoDepthAnything:
+    """Construct, load weights (reference checkpoint dict or the synthetic recipe), move to device."""
+    from .weights import synthetic_state_dict
+    m = VideoDepthAnything.from_config(encoder, device="meta")
+    if state_dict is None:
+        state_dict = synthetic_state_dict((k, tuple(v.shape)) for k, v in m.state_dict().items())
+    m.load_state_dict(state_dict, strict=True, assign=True)
+    m = m.to(device).eval()
+    return m

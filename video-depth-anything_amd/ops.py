@@ -1,0 +1,197 @@
+"""Tensor-level wrappers over the libvda C ABI.
+
+Each wrapper validates device / dtype / layout, allocates its output through the PyTorch caching
+allocator, and launches on ``torch.cuda.current_stream()`` (so whole forwards can be captured in a
+CUDA(HIP) graph).  Activations are fp16 NHWC / token-major; biases, scales and norm affines fp32.
+There is deliberately no CPU path: calling an op on a CPU tensor, or without libvda, raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib
+from ._lib import Epilogue, check, ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU, STORE_ROWS, STORE_PIXEL_SHUFFLE  # noqa: F401
+
+Tensor = torch.Tensor
+
+
+def _stream(t: Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _ptr(t: Optional[Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _need(t: Tensor, dtype, name: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"vda op: {name} must be a GPU tensor (no CPU path in the product)")
+    if t.dtype != dtype:
+        raise RuntimeError(f"vda op: {name} must be {dtype}, got {t.dtype}")
+
+
+def _need_contig(t: Tensor, dtype, name: str):
+    _need(t, dtype, name)
+    if not t.is_contiguous():
+        raise RuntimeError(f"vda op: {name} must be contiguous")
+
+
+def _epilogue(bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None, res2=None,
+              act=ACT_NONE, store=STORE_ROWS, ps=(0, 0, 0, 0)) -> Epilogue:
+    e = Epilogue()
+    for name, t in (("bias", bias), ("rowbias", rowbias), ("gamma", gamma)):
+        if t is not None:
+            _need_contig(t, torch.float32, name)
+            setattr(e, name, t.data_ptr())
+    e.rdiv, e.rmod = int(rdiv), int(rmod)
+    if res is not None:
+        _need(res, torch.float16, "res")
+        assert res.stride(-1) == 1
+        e.res, e.ldres = res.data_ptr(), res.stride(-2) if res.dim() >= 2 else res.shape[-1]
+    if res2 is not None:
+        _need(res2, torch.float16, "res2")
+        assert res2.stride(-1) == 1
+        e.res2, e.ldres2 = res2.data_ptr(), res2.stride(-2) if res2.dim() >= 2 else res2.shape[-1]
+    e.act, e.store = int(act), int(store)
+    e.ps_k, e.ps_cout, e.ps_hin, e.ps_win = (int(v) for v in ps)
+    return e
+
+
+def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
+         res2=None, act=ACT_NONE, out: Optional[Tensor] = None) -> Tensor:
+    """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view."""
+    _need(x, torch.float16, "x")
+    _need_contig(w, torch.float16, "w")
+    assert x.dim() == 2 and x.stride(1) == 1, "x must be a 2-D row-major (possibly row-strided) matrix"
+    M, K = x.shape
+    N = w.shape[0]
+    assert w.shape[1] == K, f"K mismatch {w.shape} vs {x.shape}"
+    nout = N // 2 if act == ACT_GEGLU else N
+    if out is None:
+        out = torch.empty((M, nout), dtype=torch.float16, device=x.device)
+    assert out.dim() == 2 and out.stride(1) == 1 and out.shape == (M, nout)
+    e = _epilogue(bias, rowbias, rdiv, rmod, gamma, res, res2, act)
+    rc = _lib.lib().vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0),
+                             M, N, K, e, _stream(x))
+    check(rc, "vda_gemm")
+    return out
+
+
+def conv_transpose_ks(x: Tensor, w: Tensor, bias: Tensor, BT: int, h: int, w_: int, k: int) -> Tensor:
+    """ConvTranspose2d(kernel = stride = k) as one GEMM with a pixel-shuffle store.
+    x [BT*h*w, Cin]; w [k*k*Cout, Cin] packed (i, j, co); bias [k*k*Cout] fp32 -> [BT, h*k, w*k, Cout]."""
+    _need(x, torch.float16, "x")
+    _need_contig(w, torch.float16, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    cout = N // (k * k)
+    out = torch.empty((BT, h * k, w_ * k, cout), dtype=torch.float16, device=x.device)
+    e = _epilogue(bias=bias, store=STORE_PIXEL_SHUFFLE, ps=(k, cout, h, w_))
+    rc = _lib.lib().vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), N, M, N, K, e, _stream(x))
+    check(rc, "vda_gemm(pixel-shuffle)")
+    return out
+
+
+def conv2d(x: Tensor, w: Tensor, *, ks=3, stride=1, pad=1, bias=None, pre_relu=False, act=ACT_NONE,
+           res=None, res2=None, up=None) -> Tensor:
+    """NHWC conv.  x [BT, H, W, Cin] fp16; w [Cout, ks, ks, Cin] fp16 -> [BT, Ho, Wo, Cout].
+    `up=(Hu, Wu)` reads x through a bilinear align_corners=True resize to (Hu, Wu) first."""
+    _need_contig(x, torch.float16, "x")
+    _need_contig(w, torch.float16, "w")
+    BT, H, W, Cin = x.shape
+    Cout = w.shape[0]
+    assert w.shape[1:] == (ks, ks, Cin), f"weight {tuple(w.shape)} vs Cin={Cin} ks={ks}"
+    Hi, Wi = (up if up is not None else (H, W))
+    Ho = (Hi + 2 * pad - ks) // stride + 1
+    Wo = (Wi + 2 * pad - ks) // stride + 1
+    out = torch.empty((BT, Ho, Wo, Cout), dtype=torch.float16, device=x.device)
+    r = res.reshape(-1, Cout) if res is not None else None
+    r2 = res2.reshape(-1, Cout) if res2 is not None else None
+    e = _epilogue(bias=bias, res=r, res2=r2, act=act)
+    uh, uw = (up if up is not None else (0, 0))
+    rc = _lib.lib().vda_conv2d(x.data_ptr(), w.data_ptr(), out.data_ptr(), BT, H, W, Cin, Cout, ks, stride, pad,
+                               int(bool(pre_relu)), uh, uw, e, _stream(x))
+    check(rc, "vda_conv2d")
+    return out
+
+
+def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period: int = 0,
+              rows: Optional[int] = None) -> Tensor:
+    """Row LayerNorm of x [R, C] (row-strided ok).  skip_period=np drops each frame's cls row."""
+    _need(x, torch.float16, "x")
+    _need_contig(gamma, torch.float32, "gamma")
+    _need_contig(beta, torch.float32, "beta")
+    assert x.dim() == 2 and x.stride(1) == 1
+    R, C = x.shape
+    if rows is None:
+        rows = R if skip_period == 0 else (R // (skip_period + 1)) * skip_period
+    out = torch.empty((rows, C), dtype=torch.float16, device=x.device)
+    rc = _lib.lib().vda_layernorm(x.data_ptr(), x.stride(0), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                                  rows, C, float(eps), int(skip_period), _stream(x))
+    check(rc, "vda_layernorm")
+    return out
+
+
+def groupnorm(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, eps: float) -> Tensor:
+    """GroupNorm on NHWC frames: x [F*S, C] -> same."""
+    _need_contig(x, torch.float16, "x")
+    R, C = x.shape
+    S = R // frames
+    out = torch.empty_like(x)
+    rc = _lib.lib().vda_groupnorm(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S, C,
+                                  groups, float(eps), None, _stream(x))
+    check(rc, "vda_groupnorm")
+    return out
+
+
+def spatial_attention(qkv: Tensor, B: int, N: int, H: int, D: int = 64) -> Tensor:
+    _need_contig(qkv, torch.float16, "qkv")
+    assert qkv.shape == (B * N, 3 * H * D)
+    out = torch.empty((B * N, H * D), dtype=torch.float16, device=qkv.device)
+    rc = _lib.lib().vda_spatial_attention(qkv.data_ptr(), out.data_ptr(), B, N, H, D, float(D) ** -0.5,
+                                          _stream(qkv))
+    check(rc, "vda_spatial_attention")
+    return out
+
+
+def temporal_attention(qkv: Tensor, B: int, T: int, S: int, H: int, D: int) -> Tensor:
+    _need_contig(qkv, torch.float16, "qkv")
+    assert qkv.shape == (B * T * S, 3 * H * D)
+    out = torch.empty((B * T * S, H * D), dtype=torch.float16, device=qkv.device)
+    rc = _lib.lib().vda_temporal_attention(qkv.data_ptr(), out.data_ptr(), B, T, S, H, D, float(D) ** -0.5,
+                                           _stream(qkv))
+    check(rc, "vda_temporal_attention")
+    return out
+
+
+def upsample_bilinear(x: Tensor, Ho: int, Wo: int) -> Tensor:
+    _need_contig(x, torch.float16, "x")
+    BT, H, W, C = x.shape
+    out = torch.empty((BT, Ho, Wo, C), dtype=torch.float16, device=x.device)
+    rc = _lib.lib().vda_upsample_bilinear(x.data_ptr(), out.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
+    check(rc, "vda_upsample_bilinear")
+    return out
+
+
+def patch_im2col(img: Tensor, Kp: int) -> Tensor:
+    _need_contig(img, torch.float32, "img")
+    BT, _, H, W = img.shape
+    np_ = (H // 14) * (W // 14)
+    out = torch.empty((BT * (1 + np_), Kp), dtype=torch.float16, device=img.device)
+    rc = _lib.lib().vda_patch_im2col(img.data_ptr(), out.data_ptr(), BT, H, W, Kp, _stream(img))
+    check(rc, "vda_patch_im2col")
+    return out
+
+
+def depth_head(x: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, Ho: int, Wo: int) -> Tensor:
+    _need_contig(x, torch.float16, "x")
+    for n, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2)):
+        _need_contig(t, torch.float32, n)
+    BT, H, W, C = x.shape
+    out = torch.empty((BT, Ho, Wo), dtype=torch.float32, device=x.device)
+    rc = _lib.lib().vda_depth_head(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                   out.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
+    check(rc, "vda_depth_head")
+    return out
