@@ -111,6 +111,7 @@ struct ConvLoader {
 };
 
 // ---- epilogue ------------------------------------------------------------------------------
+template <int ACT>
 __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4 v) {
   const vda_epilogue& e = p.epi;
   if (e.bias) {
@@ -122,10 +123,10 @@ __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4
     f4 b = *reinterpret_cast<const f4*>(e.rowbias + (long)r * p.N + n);
     v += b;
   }
-  if (e.act == VDA_ACT_GELU) {
+  if constexpr (ACT == VDA_ACT_GELU) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = gelu_erf(v[j]);
-  } else if (e.act == VDA_ACT_RELU) {
+  } else if constexpr (ACT == VDA_ACT_RELU) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = fmaxf(v[j], 0.f);
   }
@@ -189,7 +190,7 @@ __device__ __forceinline__ void epi_geglu4(const GemmParams& p, int m, int nh, i
 }
 
 // ---- main kernel ---------------------------------------------------------------------------
-template <int BM, int BN, class Loader>
+template <int BM, int BN, class Loader, int ACT>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
   constexpr int TM = BM / 32;  // 16-row m subtiles per wave
   constexpr int TN = BN / 32;  // 16-row n subtiles per wave
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
 
   // epilogue: lane holds D[n = 4*(lane>>4) + r][m = lane&15] of every (i, j) subtile
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
-  if (p.epi.act == VDA_ACT_GEGLU) {
+  if constexpr (ACT == VDA_ACT_GEGLU) {
 #pragma unroll
     for (int i = 0; i < TN; i += 2) {
       const int nbase = n0 + wn * (BN / 2) + i * 16;  // h block; gate block = nbase + 16
@@ -286,22 +287,31 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         int m = m0 + wm * (BM / 2) + j * 16 + mcol;
-        if (m < p.M) epi_store4(p, m, n, acc[i][j]);
+        if (m < p.M) epi_store4<ACT>(p, m, n, acc[i][j]);
       }
     }
   }
 }
 
+template <class Loader, int ACT>
+void launch_act(const GemmParams& p, hipStream_t st) {
+  // tile choice: wide tiles for big N, narrow for the DPT head's small channel counts
+  if (p.N >= 128) {
+    const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + 127) / 128;
+    hipLaunchKernelGGL((gemm_kernel<128, 128, Loader, ACT>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  } else {
+    const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + 63) / 64;
+    hipLaunchKernelGGL((gemm_kernel<128, 64, Loader, ACT>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  }
+}
+
 template <class Loader>
 int launch(const GemmParams& p, hipStream_t st) {
-  // tile choice: wide tiles for big N, narrow for the DPT head's small channel counts
-  int tiles_m, tiles_n;
-  if (p.N >= 128) {
-    tiles_m = (p.M + 127) / 128; tiles_n = (p.N + 127) / 128;
-    hipLaunchKernelGGL((gemm_kernel<128, 128, Loader>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
-  } else {
-    tiles_m = (p.M + 127) / 128; tiles_n = (p.N + 63) / 64;
-    hipLaunchKernelGGL((gemm_kernel<128, 64, Loader>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  switch (p.epi.act) {
+    case VDA_ACT_GELU: launch_act<Loader, VDA_ACT_GELU>(p, st); break;
+    case VDA_ACT_GEGLU: launch_act<Loader, VDA_ACT_GEGLU>(p, st); break;
+    case VDA_ACT_RELU: launch_act<Loader, VDA_ACT_RELU>(p, st); break;
+    default: launch_act<Loader, VDA_ACT_NONE>(p, st); break;
   }
   VDA_LAUNCH_CHECK();
   return 0;

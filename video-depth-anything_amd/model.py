@@ -438,7 +438,7 @@ class VideoDepthAnything(nn.Module):
             del qkv
             ops.gemm(at, q.proj_w, bias=q.proj_b, gamma=q.ls1, res=tok, out=tok)
             hN = ops.layernorm(tok, q.n2w, q.n2b, 1e-6)
-            f = ops.gemm(hN, q.fc1_w, bias=q.fc1_b, act=ACT_GELU)
+            f = ops.gemm(hN, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, tag="enc_fc1")
             ops.gemm(f, q.fc2_w, bias=q.fc2_b, gamma=q.ls2, res=tok, out=tok)
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)

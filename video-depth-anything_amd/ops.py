@@ -17,6 +17,27 @@ from ._lib import Epilogue, check, ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU, STOR
 Tensor = torch.Tensor
 
 
+# Optional per-launch timing of tagged launches (bench.py's roofline leg).  When a tag is enabled,
+# the launch is bracketed by two events on the launch stream; nothing else changes.
+_PROBE: Optional[dict] = None
+
+
+def enable_probe(tags):
+    global _PROBE
+    _PROBE = {t: [] for t in tags}
+
+
+def take_probe():
+    """Return {tag: [ms per launch]} for the probed launches (synchronises) and disable probing."""
+    global _PROBE
+    out = {}
+    if _PROBE:
+        torch.cuda.synchronize()
+        out = {t: [a.elapsed_time(b) for a, b in ev] for t, ev in _PROBE.items()}
+    _PROBE = None
+    return out
+
+
 def _stream(t: Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
@@ -60,7 +81,7 @@ def _epilogue(bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None, res
 
 
 def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
-         res2=None, act=ACT_NONE, out: Optional[Tensor] = None) -> Tensor:
+         res2=None, act=ACT_NONE, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
     """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view."""
     _need(x, torch.float16, "x")
     _need_contig(w, torch.float16, "w")
@@ -73,8 +94,15 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
         out = torch.empty((M, nout), dtype=torch.float16, device=x.device)
     assert out.dim() == 2 and out.stride(1) == 1 and out.shape == (M, nout)
     e = _epilogue(bias, rowbias, rdiv, rmod, gamma, res, res2, act)
+    probe = _PROBE is not None and tag in _PROBE
+    if probe:
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
     rc = _lib.lib().vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0),
                              M, N, K, e, _stream(x))
+    if probe:
+        ev1.record()
+        _PROBE[tag].append((ev0, ev1))
     check(rc, "vda_gemm")
     return out
 
