@@ -156,6 +156,12 @@ int vda_depth_head(const void* x, const float* w1, const float* b1, const float*
                    const float* b2, float* depth, int32_t BT, int32_t Hin, int32_t Win,
                    int32_t C, int32_t Ho, int32_t Wo, void* stream);
 
+/*
+ * Tuning hook: force the GEMM/conv tile configuration (-1 = automatic; 0 = 128x128/4 waves,
+ * 1 = 256x128/8 waves, 2 = 128x64/4 waves, 3 = 256x256/8 waves).  Process-global; for benchmarks.
+ */
+int vda_debug_force_tile(int32_t cfg);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libvda.so")
 EXPORTED = (
     "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
-    "vda_depth_head",
+    "vda_depth_head", "vda_debug_force_tile",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -61,6 +61,7 @@ def _declare(lib):
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),
         "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
         "vda_depth_head": ([P, P, P, P, P, P, I, I, I, I, I, I, P], I),
+        "vda_debug_force_tile": ([I], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)

@@ -189,9 +189,9 @@ __device__ __forceinline__ void epi_geglu4(const GemmParams& p, int m, int nh, i
   *reinterpret_cast<h4*>(p.y + (long)m * p.ldy + n_out) = o;
 }
 
-// ---- main kernel ---------------------------------------------------------------------------
+// ---- register-staged kernel (conv with a fused bilinear-upsample loader) ----------------------
 template <int BM, int BN, class Loader, int ACT>
-__global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
+__global__ __launch_bounds__(256) void gemm_reg_kernel(GemmParams p, int tiles_n) {
   constexpr int TM = BM / 32;  // 16-row m subtiles per wave
   constexpr int TN = BN / 32;  // 16-row n subtiles per wave
   constexpr int XIT = BM / 32; // 16-B chunks per thread for the X tile (BM*8 / 256)
@@ -293,25 +293,226 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmParams p, int tiles_n) {
   }
 }
 
-template <class Loader, int ACT>
-void launch_act(const GemmParams& p, hipStream_t st) {
-  // tile choice: wide tiles for big N, narrow for the DPT head's small channel counts
-  if (p.N >= 128) {
-    const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + 127) / 128;
-    hipLaunchKernelGGL((gemm_kernel<128, 128, Loader, ACT>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+// ---- LDS-DMA kernel (every dense GEMM and plain conv) ------------------------------------------
+// Operand tiles are moved HBM -> LDS with global_load_lds_dwordx4 (no VGPR staging): one wave
+// instruction fills 8 rows x 128 B of the [BM + BN][64] tile (X rows first, then W rows).  The DMA
+// destination is lane-linear, so the (row>>1)&7 chunk swizzle is applied to the per-lane SOURCE
+// address.  Lanes whose source is out of range (rows >= M / N, k >= K, conv zero padding) read a
+// zero page instead, so no predication reaches the LDS image.  Two LDS buffers, BK = 64: tile t+1
+// is issued before the MFMAs of tile t and drained by the barrier that ends tile t.
+// Block -> tile mapping is XCD-aware: the 8 XCDs each take a contiguous run of tiles, grouped
+// GROUP_M m-panels at a time so co-resident blocks share X panels and W tiles in their XCD's L2.
+__device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
+
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GROUP_M * tiles_n;
+  const int group = wgid / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsize = min(tiles_m - first_m, GROUP_M);
+  const int in_group = wgid - group * per_group;
+  tm = first_m + in_group % gsize;
+  tn = in_group / gsize;
+}
+
+__device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
+}
+
+template <int BM, int BN, int NWM, int NWN, bool CONV, int ACT>
+__global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int NW = NWM * NWN;
+  constexpr int WTM = BM / NWM, WTN = BN / NWN;  // wave tile
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int ROWS = BM + BN;
+  constexpr int GROUPS = ROWS / 8;               // 1-KiB DMA pieces per tile
+  static_assert(GROUPS % NW == 0, "pieces must divide evenly over the waves");
+  constexpr int IPW = GROUPS / NW;               // DMA instructions per wave per tile
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * ROWS * BK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % NWM, wn = wave / NWM;
+  int tile_m, tile_n;
+  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, tile_m, tile_n);
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // per-lane source descriptors for this wave's IPW pieces
+  const h16* rowp[IPW];
+  int kch[IPW];        // logical k offset (halfs) of this lane's chunk within the K tile
+  bool isx[IPW];
+  int cbt[IPW], coy[IPW], cox[IPW];
+  bool rowok[IPW];
+#pragma unroll
+  for (int i = 0; i < IPW; ++i) {
+    const int g = wave * IPW + i;
+    const int R = g * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((R >> 1) & 7);
+    kch[i] = c * 8;
+    isx[i] = R < BM;
+    if (R < BM) {
+      const int m = m0 + R;
+      rowok[i] = m < p.M;
+      if constexpr (CONV) {
+        const int mm = rowok[i] ? m : 0;
+        cox[i] = mm % p.Wo;
+        const int t = mm / p.Wo;
+        coy[i] = t % p.Ho;
+        cbt[i] = t / p.Ho;
+        rowp[i] = p.x;
+      } else {
+        rowp[i] = p.x + (long)(rowok[i] ? m : 0) * p.ldx;
+      }
+    } else {
+      const int n = n0 + R - BM;
+      rowok[i] = n < p.N;
+      rowp[i] = p.w + (long)(rowok[i] ? n : 0) * p.K;
+    }
+  }
+  const void* zero = (const void*)g_zero_page;
+
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int i = 0; i < IPW; ++i) {
+      const int k = k0 + kch[i];
+      const void* src = zero;
+      if (rowok[i] && k < p.K) {
+        if (CONV && isx[i]) {
+          const int tap = k / p.Cin, ci = k - tap * p.Cin;
+          const int ky = tap / p.ks, kx = tap - ky * p.ks;
+          const int iy = coy[i] * p.stride - p.pad + ky, ix = cox[i] * p.stride - p.pad + kx;
+          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+            src = p.x + (((long)cbt[i] * p.H + iy) * p.W + ix) * p.Cin + ci;
+        } else {
+          src = rowp[i] + k;
+        }
+      }
+      glds16(src, smem + buf * ROWS * BK + (wave * IPW + i) * 8 * BK);
+    }
+  };
+
+  f4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  issue(0, 0);
+  __syncthreads();
+  const int frow = lane & 15, fchunk = lane >> 4;
+  const bool prerelu = CONV && p.pre_relu;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) issue((kt + 1) * BK, buf ^ 1);
+    const h16* sX = smem + buf * ROWS * BK;
+    const h16* sW = sX + BM * BK;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      h8 af[TN], bf[TM];
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+        af[i] = *reinterpret_cast<const h8*>(&sW[swz(wn * WTN + i * 16 + frow, ks * 4 + fchunk)]);
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        bf[j] = *reinterpret_cast<const h8*>(&sX[swz(wm * WTM + j * 16 + frow, ks * 4 + fchunk)]);
+        if (prerelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bf[j][e] = bf[j][e] > (h16)0 ? bf[j][e] : (h16)0;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  const int mcol = lane & 15, nq = (lane >> 4) * 4;
+  if constexpr (ACT == VDA_ACT_GEGLU) {
+    static_assert(TN % 2 == 0, "GEGLU needs an even number of n subtiles per wave");
+#pragma unroll
+    for (int i = 0; i < TN; i += 2) {
+      const int nbase = n0 + wn * WTN + i * 16;
+      if (nbase >= p.N) continue;
+      const int n_out = (nbase >> 1) + nq;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * WTM + j * 16 + mcol;
+        if (m < p.M) epi_geglu4(p, m, nbase + nq, nbase + 16 + nq, n_out, acc[i][j], acc[i + 1][j]);
+      }
+    }
   } else {
-    const int tiles_m = (p.M + 127) / 128, tiles_n = (p.N + 63) / 64;
-    hipLaunchKernelGGL((gemm_kernel<128, 64, Loader, ACT>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int n = n0 + wn * WTN + i * 16 + nq;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int m = m0 + wm * WTM + j * 16 + mcol;
+        if (m < p.M) epi_store4<ACT>(p, m, n, acc[i][j]);
+      }
+    }
   }
 }
 
-template <class Loader>
+int g_force_tile = -1;  // debug / tuning override (vda_debug_force_tile)
+
+template <int BM, int BN, int NWM, int NWN, bool CONV, int ACT>
+void launch_tile(const GemmParams& p, hipStream_t st) {
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, NWM, NWN, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(NWM * NWN * 64), 0, st,
+                     p, tiles_m, tiles_n);
+}
+
+template <bool CONV, int ACT>
+void launch_act(const GemmParams& p, hipStream_t st) {
+  int cfg = g_force_tile;
+  if (cfg < 0) {
+    // measured on MI355X (tools/bench_gemm.py): 256x256 wins every large-N shape; N = 128 prefers
+    // 256x128; short K (<= 256) and narrow N prefer the 2-blocks-per-CU 128x64 tile.
+    if (p.N <= 64 || p.K <= 256) cfg = 2;
+    else if (p.N >= 256 && p.M >= 4096) cfg = 3;
+    else if (p.N >= 128 && p.M >= 4096) cfg = 1;
+    else cfg = 0;
+  }
+  switch (cfg) {
+    case 1: launch_tile<256, 128, 4, 2, CONV, ACT>(p, st); break;
+    case 2: launch_tile<128, 64, 2, 2, CONV, ACT>(p, st); break;
+    case 3: launch_tile<256, 256, 2, 4, CONV, ACT>(p, st); break;
+    default: launch_tile<128, 128, 2, 2, CONV, ACT>(p, st); break;
+  }
+}
+
+template <bool CONV>
 int launch(const GemmParams& p, hipStream_t st) {
   switch (p.epi.act) {
-    case VDA_ACT_GELU: launch_act<Loader, VDA_ACT_GELU>(p, st); break;
-    case VDA_ACT_GEGLU: launch_act<Loader, VDA_ACT_GEGLU>(p, st); break;
-    case VDA_ACT_RELU: launch_act<Loader, VDA_ACT_RELU>(p, st); break;
-    default: launch_act<Loader, VDA_ACT_NONE>(p, st); break;
+    case VDA_ACT_GELU: launch_act<CONV, VDA_ACT_GELU>(p, st); break;
+    case VDA_ACT_GEGLU: launch_act<CONV, VDA_ACT_GEGLU>(p, st); break;
+    case VDA_ACT_RELU: launch_act<CONV, VDA_ACT_RELU>(p, st); break;
+    default: launch_act<CONV, VDA_ACT_NONE>(p, st); break;
+  }
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_reg_conv(const GemmParams& p, hipStream_t st) {
+  const int tiles_m = (p.M + 127) / 128;
+  if (p.N >= 128) {
+    const int tiles_n = (p.N + 127) / 128;
+    if (p.epi.act == VDA_ACT_RELU)
+      hipLaunchKernelGGL((gemm_reg_kernel<128, 128, ConvLoader, VDA_ACT_RELU>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+    else
+      hipLaunchKernelGGL((gemm_reg_kernel<128, 128, ConvLoader, VDA_ACT_NONE>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+  } else {
+    const int tiles_n = (p.N + 63) / 64;
+    if (p.epi.act == VDA_ACT_RELU)
+      hipLaunchKernelGGL((gemm_reg_kernel<128, 64, ConvLoader, VDA_ACT_RELU>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
+    else
+      hipLaunchKernelGGL((gemm_reg_kernel<128, 64, ConvLoader, VDA_ACT_NONE>), dim3(tiles_m * tiles_n), dim3(256), 0, st, p, tiles_n);
   }
   VDA_LAUNCH_CHECK();
   return 0;
@@ -353,7 +554,7 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
   int rc = check_epi(p.epi, N);
   if (rc) return rc;
-  return launch<DenseLoader>(p, (hipStream_t)stream);
+  return launch<false>(p, (hipStream_t)stream);
 }
 
 extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
@@ -377,8 +578,15 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   p.epi = epi ? *epi : default_epi();
   if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
-  VDA_CHECK_ARG(p.epi.store == VDA_STORE_ROWS && p.epi.act != VDA_ACT_GEGLU, "conv: row store, no GEGLU");
+  VDA_CHECK_ARG(p.epi.store == VDA_STORE_ROWS && (p.epi.act == VDA_ACT_NONE || p.epi.act == VDA_ACT_RELU),
+                "conv: row store, activation none/relu");
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
-  return launch<ConvLoader>(p, (hipStream_t)stream);
+  if (p.up_h > 0) return launch_reg_conv(p, (hipStream_t)stream);
+  return launch<true>(p, (hipStream_t)stream);
+}
+
+extern "C" int vda_debug_force_tile(int32_t cfg) {
+  g_force_tile = cfg;
+  return 0;
 }
