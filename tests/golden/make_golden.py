@@ -45,7 +45,17 @@ def import_reference():
     sys.path.insert(0, REF)
     ed = types.ModuleType("easydict"); ed.EasyDict = dict; sys.modules["easydict"] = ed
     cv2 = types.ModuleType("cv2"); cv2.INTER_CUBIC, cv2.INTER_AREA, cv2.INTER_NEAREST = 2, 3, 0
+
+    def resize(img, dsize, interpolation=None):
+        # stand-in for cv2.resize(INTER_CUBIC) used only by the video case: torch bicubic
+        # (a = -0.75, the same kernel); the windowing/stitching logic is what that case pins.
+        w, h = dsize
+        t = torch.from_numpy(np.ascontiguousarray(img, dtype=np.float32)).permute(2, 0, 1)[None]
+        t = torch.nn.functional.interpolate(t, size=(h, w), mode="bicubic", align_corners=False)
+        return t[0].permute(1, 2, 0).numpy()
+    cv2.resize = resize
     sys.modules["cv2"] = cv2
+    tq = types.ModuleType("tqdm"); tq.tqdm = lambda it, *a, **k: it; sys.modules.setdefault("tqdm", tq)
     tv = types.ModuleType("torchvision"); tvt = types.ModuleType("torchvision.transforms")
 
     class Compose:
@@ -89,6 +99,20 @@ def main():
                             tap_stats=np.array(taps, dtype=np.float64),
                             meta=np.array(json.dumps(dict(encoder=enc, B=B, T=T, H=H, W=Wd, skip_tmp_block=skip))))
         print(name, tuple(d.shape), float(d.mean()), float(d.min()), float(d.max()), flush=True)
+    # long-video windowing + stitching (video_depth.py:329-417): 57 frames -> 3 windows
+    g = torch.Generator().manual_seed(99)
+    base = torch.rand(1, 3, 8, 10, generator=g)
+    frames = []
+    for t in range(57):  # a smoothly drifting synthetic scene, uint8 RGB 48x64
+        f = torch.nn.functional.interpolate(torch.roll(base, shifts=t // 6, dims=3), size=(48, 64), mode="bilinear",
+                                            align_corners=False)
+        frames.append((f[0].permute(1, 2, 0) * 255).clamp(0, 255).to(torch.uint8).numpy())
+    frames = np.stack(frames)
+    with torch.no_grad():
+        depth, fps = models["vits"].infer_video_depth(frames, 24, input_size=56, device="cpu", fp32=True)
+    np.savez_compressed(os.path.join(HERE, "video_vits_57f.npz"), frames=frames, depth=depth.astype(np.float32),
+                        meta=np.array(json.dumps(dict(encoder="vits", input_size=56, fps=fps))))
+    print("video_vits_57f", depth.shape, float(depth.mean()), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,77 @@
+"""The C-ABI library: loads, exports exactly what include/vda.h declares, validates arguments.
+
+CPU-only: the argument checks run before any HIP call, so they are exercised without a GPU.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import vda_amd
+from vda_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "vda.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(vda_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_lists_match_binding():
+    assert header_functions() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libvda.so not built")
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (vda_[a-z0-9_]+)", out))
+    missing = [f for f in header_functions() if f not in exported]
+    assert not missing, missing
+
+
+def test_version_and_error_plumbing():
+    lib = _lib.lib()
+    assert b"gfx950" in lib.vda_version()
+    e = _lib.Epilogue()
+    rc = lib.vda_gemm(None, 8, None, None, 8, 1, 4, 8, e, None)
+    assert rc == -22
+    assert b"null pointer" in lib.vda_last_error()
+
+
+@pytest.mark.parametrize("args,msg", [
+    ((16, 0, 16, 4, 16), b"empty GEMM"),      # M, N, K, ldx/ldy variations
+    ((16, 4, 12, 4, 16), b"multiples of 8"),  # K % 8
+    ((16, 6, 16, 6, 16), b"multiples of 4"),  # N % 4
+])
+def test_gemm_argument_validation(args, msg):
+    lib = _lib.lib()
+    M, N, K, ldy, ldx = args
+    fake = ctypes.c_void_p(0x1000)
+    rc = lib.vda_gemm(fake, ldx, fake, fake, ldy, M, N, K, _lib.Epilogue(), None)
+    assert rc == -22
+    assert msg in lib.vda_last_error()
+
+
+def test_conv_and_attention_validation():
+    lib = _lib.lib()
+    fake = ctypes.c_void_p(0x1000)
+    e = _lib.Epilogue()
+    assert lib.vda_conv2d(fake, fake, fake, 1, 8, 8, 12, 16, 3, 1, 1, 0, 0, 0, e, None) == -22  # Cin % 8
+    assert lib.vda_spatial_attention(fake, fake, 1, 10, 2, 32, 0.1, None) == -22                # D != 64
+    assert lib.vda_temporal_attention(fake, fake, 1, 33, 4, 8, 16, 0.1, None) == -22          # T > 32
+    assert b"T <= 32" in lib.vda_last_error()
+    assert lib.vda_patch_im2col(fake, fake, 1, 20, 28, 592, None) == -22                      # H % 14
+    assert b"multiples of the patch size" in lib.vda_last_error()
+
+
+def test_model_refuses_cpu_input():
+    import torch
+    m = vda_amd.VideoDepthAnything.from_config("vits", device="meta")
+    with pytest.raises(RuntimeError, match="GPU only"):
+        m(torch.zeros(1, 2, 3, 28, 28))

@@ -1,0 +1,121 @@
+"""Long-video orchestration (video_depth.py:329-417): windows, stitching, clip-parallel sharding.
+
+CPU tests drive ``vda_amd.video.infer_video_depth`` with the oracle as the clip forward and
+compare with the reference's own ``infer_video_depth`` output (tests/golden/video_vits_57f.npz);
+the world-size-2 gloo test checks that sharding windows over ranks + gather reproduces the
+single-process result exactly.  The GPU test runs the same video through libvda.
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from helpers import GOLDEN, recipe_state_dict, vda_oracle
+from vda_amd import video as V
+
+
+def load_video_golden():
+    z = np.load(os.path.join(GOLDEN, "video_vits_57f.npz"), allow_pickle=False)
+    return z["frames"], z["depth"], json.loads(str(z["meta"]))
+
+
+def simulate_reference_windows(n):
+    """Literal replay of the reference loop (video_depth.py:351-364) on frame ids."""
+    step = V.INFER_LEN - V.OVERLAP
+    plist = list(range(n)) + [n - 1] * ((step - n % step) % step + (V.INFER_LEN - step))
+    wins, pre = [], None
+    for fid in range(0, n, step):
+        cur = [plist[fid + i] for i in range(V.INFER_LEN)]
+        if pre is not None:
+            cur[:V.OVERLAP] = [pre[j] for j in V.KEYFRAMES]
+        wins.append(cur)
+        pre = cur
+    return wins, len(plist)
+
+
+@pytest.mark.parametrize("n", [1, 5, 22, 23, 32, 44, 57, 100, 447])
+def test_window_closed_form_matches_reference_loop(n):
+    wins, plen = simulate_reference_windows(n)
+    assert plen == V.padded_length(n)
+    assert len(wins) == len(V.window_starts(n))
+    for k, w in enumerate(wins):
+        assert V.window_frame_indices(k, n) == w
+
+
+def test_net_input_size_rules():
+    assert V.net_input_size(48, 64, 56) == (56, 70)
+    assert V.net_input_size(720, 1280, 518) == (518, 924)  # 16:9 < 1.78: no shrink
+    assert V.net_input_size(280, 924, 518) == (280, 924)   # ratio 3.3 > 1.78: input_size shrinks to 280
+    for h, w in [(480, 640), (1080, 1920), (100, 37)]:
+        H, W = V.net_input_size(h, w, 518)
+        assert H % 14 == 0 and W % 14 == 0
+
+
+def _oracle_forward(sd):
+    return lambda x: vda_oracle.forward(sd, "vits", x.cpu())
+
+
+def test_video_orchestration_matches_reference_golden():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    frames, depth_ref, meta = load_video_golden()
+    sd = recipe_state_dict("vits")
+    depth, fps = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
+                                     device="cpu")
+    assert depth.shape == depth_ref.shape
+    err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
+    assert err <= 1e-5, err
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+    frames, _, meta = load_video_golden()
+    sd = recipe_state_dict("vits")
+    depth, _ = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
+                                   device="cpu", rank=rank, world=world)
+    if rank == 0:
+        q.put(depth)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_clip_parallel_gloo_world2_matches_single_process():
+    frames, depth_ref, meta = load_video_golden()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    depth = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
+    assert err <= 1e-5, err
+
+
+@pytest.mark.gpu
+def test_video_on_gpu_matches_reference_golden():
+    import vda_amd
+    frames, depth_ref, meta = load_video_golden()
+    m = vda_amd.build_model("vits", recipe_state_dict("vits"), device="cuda")
+    depth, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda",
+                                   windows_per_batch=2)
+    err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
+    print(f"video 57 frames: rel-L1 vs reference = {err:.3e}")
+    assert err <= 1e-3, err

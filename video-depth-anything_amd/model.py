@@ -491,6 +491,22 @@ class VideoDepthAnything(nn.Module):
         return depth.view(B, T, H, W)
 
 
+def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", fp32=False, skip_tmp_block=False,
+                       windows_per_batch=1, rank=0, world=1, group=None):
+    """video_depth.py:329-417 on the MI355X forward (see vda_amd.video).  ``fp32=True`` is not on
+    the accelerated path (fp16 compute is the shipped mode); it raises instead of silently
+    running something else."""
+    if fp32:
+        raise NotImplementedError("fp32 inference is not implemented on the MI355X path (fp16 compute, fp32 tail)")
+    from .video import infer_video_depth
+    return infer_video_depth(lambda x: self.forward(x, skip_tmp_block), frames, target_fps, input_size=input_size,
+                             device=device, windows_per_batch=windows_per_batch, rank=rank, world=world,
+                             group=group)
+
+
+VideoDepthAnything.infer_video_depth = _infer_video_depth
+
+
 def build_model(encoder: str = "vitl", state_dict: Optional[dict] = None, device="cuda") -> VideoDepthAnything:
     """Construct, load weights (reference checkpoint dict or the synthetic recipe), move to device."""
     from .weights import synthetic_state_dict
