@@ -147,13 +147,16 @@ int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W
                      void* stream);
 
 /*
- * Depth head tail in fp32 (dpt_temporal.py:92-99, dpt.py:118-124, video_depth.py:63-64):
- * X [BT, Hin, Win, C] half (output_conv1 result) is bilinearly resized (align_corners=True) to
- * [Ho, Wo], then conv3x3(C->32, w1 [32,3,3,C] float, b1) -> ReLU -> conv1x1(32->1, w2 [32], b2)
- * -> ReLU, all in fp32.  depth [BT, Ho, Wo] float.  C % 8 == 0, C <= 256.
+ * Depth head tail (dpt_temporal.py:92-99, dpt.py:118-124, video_depth.py:63-64):
+ * X [BT, Hin, Win, C] half (the output_conv1 result) is bilinearly resized (align_corners=True,
+ * fp16 storage like the reference's autocast interpolate) into the caller's workspace
+ * ws [BT, Ho, Wo, C] half, then conv3x3(C -> 32, +b1) -> ReLU -> conv1x1(32 -> 1, w2, +b2) -> ReLU.
+ * The 3x3 conv keeps fp32 weights as an exact fp16 hi/lo split: w1 is half [64, 3, 3, C] with
+ * rows 0..31 = fp16(w) and rows 32..63 = fp16(w - fp16(w)); both halves accumulate in fp32.
+ * depth [BT, Ho, Wo] float.  C % 8 == 0.
  */
-int vda_depth_head(const void* x, const float* w1, const float* b1, const float* w2,
-                   const float* b2, float* depth, int32_t BT, int32_t Hin, int32_t Win,
+int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2,
+                   const float* b2, float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win,
                    int32_t C, int32_t Ho, int32_t Wo, void* stream);
 
 /*

@@ -206,11 +206,16 @@ def test_depth_head_fp32():
     x = rnd(BT, C, Hin, Win, seed=45)
     w1, b1 = rnd(32, C, 3, 3, scale=(9 * C) ** -0.5, seed=46), rnd(32, scale=0.1, seed=47)
     w2, b2 = rnd(1, 32, 1, 1, seed=48).abs() * 0.2, torch.tensor([0.05])
+    w1 = torch.randn(32, C, 3, 3, generator=torch.Generator().manual_seed(46)) * (9 * C) ** -0.5  # full fp32 weights
     up = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=True)
     ref = F.relu(F.conv2d(F.relu(F.conv2d(up, w1, b1, padding=1)), w2, b2))[:, 0]
-    y = ops.depth_head(h(x.permute(0, 2, 3, 1)), f32(w1.permute(0, 2, 3, 1)), f32(b1), f32(w2.reshape(-1)), f32(b2),
+    wn = w1.permute(0, 2, 3, 1)
+    split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0)
+    y = ops.depth_head(h(x.permute(0, 2, 3, 1)), split.to(DEV).contiguous(), f32(b1), f32(w2.reshape(-1)), f32(b2),
                        Ho, Wo)
-    assert rel(y, ref) < 1e-5  # fp32 path on fp16-exact inputs
+    # the resized map is stored in fp16 (as the reference's autocast interpolate does); the conv
+    # itself keeps the fp32 weights (hi/lo split) with fp32 accumulation
+    assert rel(y, ref) < 5e-4
 
 
 def test_ops_reject_cpu_tensors():

@@ -60,7 +60,7 @@ def _declare(lib):
         "vda_temporal_attention": ([P, P, I, I, I, I, I, F, P], I),
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),
         "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
-        "vda_depth_head": ([P, P, P, P, P, P, I, I, I, I, I, I, P], I),
+        "vda_depth_head": ([P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_debug_force_tile": ([I], I),
     }
     for name, (args, res) in sig.items():

@@ -305,6 +305,7 @@ __global__ __launch_bounds__(256) void gemm_reg_kernel(GemmParams p, int tiles_n
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
 constexpr int GROUP_M = 8;
+constexpr int ACT_DEPTH = 4;  // internal: depth-head tail epilogue (vda_depth_head)
 
 __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
@@ -432,7 +433,31 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
   }
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
-  if constexpr (ACT == VDA_ACT_GEGLU) {
+  if constexpr (ACT == ACT_DEPTH) {
+    // depth tail (dpt.py:118-124): the wave owns all 64 W rows = 32 output channels as fp16
+    // hi (rows 0..31) + lo (rows 32..63) halves of the fp32 weights, so y = acc_hi + acc_lo is the
+    // fp32-weight conv.  Then +b1, ReLU, 1x1 (32 -> 1) dot, +b2, ReLU; fp32 depth per pixel.
+    static_assert(TN == 4 && NWN == 1, "depth epilogue needs the whole 64-row W tile per wave");
+    const float* b1 = p.epi.bias;
+    const float* w2 = p.epi.gamma;
+    const float b2 = p.epi.rowbias[0];
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      float part = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = i * 16 + nq + r;
+          const float y = acc[i][j][r] + acc[i + 2][j][r] + b1[c];
+          part += fmaxf(y, 0.f) * w2[c];
+        }
+      part += __shfl_xor(part, 16, 64);
+      part += __shfl_xor(part, 32, 64);
+      const int m = m0 + wm * WTM + j * 16 + mcol;
+      if (lane < 16 && m < p.M) reinterpret_cast<float*>(p.y)[m] = fmaxf(part + b2, 0.f);
+    }
+  } else if constexpr (ACT == VDA_ACT_GEGLU) {
     static_assert(TN % 2 == 0, "GEGLU needs an even number of n subtiles per wave");
 #pragma unroll
     for (int i = 0; i < TN; i += 2) {
@@ -584,6 +609,31 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   if (rc) return rc;
   if (p.up_h > 0) return launch_reg_conv(p, (hipStream_t)stream);
   return launch<true>(p, (hipStream_t)stream);
+}
+
+extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
+                              float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho,
+                              int32_t Wo, void* stream) {
+  VDA_CHECK_ARG(x && w1 && b1 && w2 && b2 && depth && ws, "null pointer");
+  VDA_CHECK_ARG(BT > 0 && Hin > 0 && Win > 0 && Ho > 0 && Wo > 0, "bad depth-head geometry");
+  VDA_CHECK_ARG(C % 8 == 0, "depth head needs C % 8 == 0");
+  hipStream_t st = (hipStream_t)stream;
+  // 1) bilinear (align_corners=True) resize of the output_conv1 map to (Ho, Wo), fp16 like the
+  //    reference's autocast interpolate (dpt_temporal.py:92-94)
+  int rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
+  if (rc) return rc;
+  // 2) 3x3 conv C -> 32 with split-fp16 weights + fused ReLU / 1x1 / ReLU epilogue
+  GemmParams p{};
+  p.x = (const h16*)ws; p.w = (const h16*)w1; p.y = (h16*)depth;
+  p.H = Ho; p.W = Wo; p.Cin = C; p.ks = 3; p.stride = 1; p.pad = 1; p.pre_relu = 0;
+  p.Ho = Ho; p.Wo = Wo;
+  p.M = BT * Ho * Wo; p.N = 64; p.K = 9 * C; p.ldy = 1;
+  p.epi = default_epi();
+  p.epi.bias = b1; p.epi.gamma = w2; p.epi.rowbias = b2;
+  const int tiles_m = (p.M + 127) / 128;
+  hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, true, ACT_DEPTH>), dim3(tiles_m), dim3(256), 0, st, p, tiles_m, 1);
+  VDA_LAUNCH_CHECK();
+  return 0;
 }
 
 extern "C" int vda_debug_force_tile(int32_t cfg) {

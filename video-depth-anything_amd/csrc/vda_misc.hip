@@ -1,4 +1,4 @@
-// Bilinear resize, patch-embed im2col, the fp32 depth-head tail, and the C-ABI error plumbing.
+// Bilinear resize, patch-embed im2col, and the C-ABI error plumbing.
 #include "vda_common.h"
 #include "../../include/vda.h"
 #include <cstdio>
@@ -89,79 +89,6 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ i
   }
 }
 
-// Depth-head tail, fp32.  Block = 16x16 output pixels of one frame, one pixel per thread.
-// For each 16-channel slice of the input: the 18x18 halo of the bilinearly upsampled map is built
-// in LDS (fp32), then every thread accumulates its 3x3 x 16 x 32 products.  Weights are
-// wave-uniform (scalar loads).  Finally ReLU, 1x1 (32 -> 1), ReLU.
-constexpr int DT = 16;           // output tile edge
-constexpr int DH = DT + 2;       // halo edge
-constexpr int DCS = 16;          // channel slice
-__global__ __launch_bounds__(256) void depth_head_kernel(const h16* __restrict__ x, const float* __restrict__ w1,
-                                                         const float* __restrict__ b1, const float* __restrict__ w2,
-                                                         const float* __restrict__ b2, float* __restrict__ depth,
-                                                         int Hin, int Win, int C, int Ho, int Wo) {
-  __shared__ float tile[DH * DH][DCS + 1];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int ox0 = blockIdx.x * DT, oy0 = blockIdx.y * DT, bt = blockIdx.z;
-  const h16* xb = x + (long)bt * Hin * Win * C;
-  float acc[32];
-#pragma unroll
-  for (int co = 0; co < 32; ++co) acc[co] = b1[co];
-
-  for (int c0 = 0; c0 < C; c0 += DCS) {
-    // build halo: DH*DH pixels x 16 channels (two 8-channel chunks per pixel)
-    for (int i = threadIdx.x; i < DH * DH * 2; i += 256) {
-      const int pix = i >> 1, half = i & 1;
-      const int hy = pix / DH, hx = pix - hy * DH;
-      const int uy = oy0 - 1 + hy, ux = ox0 - 1 + hx;  // coordinate on the upsampled grid
-      float v[8];
-      if (uy < 0 || uy >= Ho || ux < 0 || ux >= Wo) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.f;
-      } else {
-        int y0, y1, x0, x1; float wy, wx;
-        ac_coord(uy, Hin, Ho, y0, y1, wy);
-        ac_coord(ux, Win, Wo, x0, x1, wx);
-        const int c = c0 + half * 8;
-        const h8 a = __builtin_bit_cast(h8, ldg16(xb + ((long)y0 * Win + x0) * C + c));
-        const h8 bb = __builtin_bit_cast(h8, ldg16(xb + ((long)y0 * Win + x1) * C + c));
-        const h8 cc = __builtin_bit_cast(h8, ldg16(xb + ((long)y1 * Win + x0) * C + c));
-        const h8 d = __builtin_bit_cast(h8, ldg16(xb + ((long)y1 * Win + x1) * C + c));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float top = (1.f - wx) * (float)a[j] + wx * (float)bb[j];
-          const float bot = (1.f - wx) * (float)cc[j] + wx * (float)d[j];
-          v[j] = (1.f - wy) * top + wy * bot;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tile[pix][half * 8 + j] = v[j];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const float* tp = tile[(ty + ky) * DH + tx + kx];
-        const float* wp = w1 + ((ky * 3 + kx) * C + c0);  // w1 layout [32][3][3][C]
-#pragma unroll 4
-        for (int ci = 0; ci < DCS; ++ci) {
-          const float v = tp[ci];
-#pragma unroll
-          for (int co = 0; co < 32; ++co) acc[co] = fmaf(v, wp[(long)co * 9 * C + ci], acc[co]);
-        }
-      }
-    __syncthreads();
-  }
-  const int oy = oy0 + ty, ox = ox0 + tx;
-  if (oy < Ho && ox < Wo) {
-    float d = b2[0];
-#pragma unroll
-    for (int co = 0; co < 32; ++co) d = fmaf(fmaxf(acc[co], 0.f), w2[co], d);
-    depth[((long)bt * Ho + oy) * Wo + ox] = fmaxf(d, 0.f);
-  }
-}
-
 }  // namespace
 
 extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t H, int32_t W, int32_t C,
@@ -189,15 +116,3 @@ extern "C" int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H
   return 0;
 }
 
-extern "C" int vda_depth_head(const void* x, const float* w1, const float* b1, const float* w2, const float* b2,
-                              float* depth, int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo,
-                              void* stream) {
-  VDA_CHECK_ARG(x && w1 && b1 && w2 && b2 && depth, "null pointer");
-  VDA_CHECK_ARG(BT > 0 && Hin > 0 && Win > 0 && Ho > 0 && Wo > 0, "bad depth-head geometry");
-  VDA_CHECK_ARG(C % DCS == 0 && C <= 1024, "depth head needs C % 16 == 0");
-  dim3 grid((Wo + DT - 1) / DT, (Ho + DT - 1) / DT, BT);
-  hipLaunchKernelGGL(depth_head_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)x, w1, b1, w2, b2,
-                     depth, Hin, Win, C, Ho, Wo);
-  VDA_LAUNCH_CHECK();
-  return 0;
-}

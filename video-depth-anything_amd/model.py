@@ -315,7 +315,10 @@ class VideoDepthAnything(nn.Module):
             P.ref[i] = q
         P.oc1_w, P.oc1_b = _conv_nhwc(s.output_conv1.weight).to(dev), _f(s.output_conv1.bias).to(dev)
         oc2 = s.output_conv2
-        P.oc2_w1 = _f(oc2[0].weight.permute(0, 2, 3, 1)).to(dev)  # [32, 3, 3, C] fp32
+        w1 = oc2[0].weight.detach().float().permute(0, 2, 3, 1)  # [32, 3, 3, C]
+        w1_hi = w1.half()
+        w1_lo = (w1 - w1_hi.float()).half()  # exact fp16 hi/lo split of the fp32 weights
+        P.oc2_w1 = torch.cat([w1_hi, w1_lo], 0).contiguous().to(dev)  # [64, 3, 3, C] fp16
         P.oc2_b1 = _f(oc2[0].bias).to(dev)
         P.oc2_w2 = _f(oc2[2].weight.reshape(-1)).to(dev)
         P.oc2_b2 = _f(oc2[2].bias).to(dev)
@@ -483,9 +486,9 @@ class VideoDepthAnything(nn.Module):
         p2 = ops.upsample_bilinear(y, r1.shape[1], r1.shape[2])
         y, _ = self._fusion(P.ref[1], p2, r1, None)  # refinenet1: scale_factor 2
         H1, W1 = 2 * y.shape[1], 2 * y.shape[2]
-        # output_conv1 on the x2 bilinear upsample, read through the conv's loader (no 296² tensor)
-        o1 = ops.conv2d(y, P.oc1_w, bias=P.oc1_b, up=(H1, W1))
-        # output_conv2 in fp32 on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
+        # refinenet1's x2 bilinear upsample (blocks.py:151-158) materialised once, then output_conv1
+        o1 = ops.conv2d(ops.upsample_bilinear(y, H1, W1), P.oc1_w, bias=P.oc1_b)
+        # output_conv2 with fp32 weights on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
         # the final resize to (H, W) is the identity because H = 14ph, W = 14pw (video_depth.py:63)
         depth = ops.depth_head(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
         return depth.view(B, T, H, W)

@@ -213,13 +213,18 @@ def patch_im2col(img: Tensor, Kp: int) -> Tensor:
     return out
 
 
-def depth_head(x: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, Ho: int, Wo: int) -> Tensor:
+def depth_head(x: Tensor, w1_split: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, Ho: int, Wo: int) -> Tensor:
+    """Depth tail: bilinear resize to (Ho, Wo), 3x3 conv (split-fp16 fp32 weights) -> ReLU -> 1x1 -> ReLU.
+    x [BT, H, W, C] fp16; w1_split [64, 3, 3, C] fp16 (hi rows 0..31, lo rows 32..63) -> depth [BT, Ho, Wo] fp32."""
     _need_contig(x, torch.float16, "x")
-    for n, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2)):
+    _need_contig(w1_split, torch.float16, "w1_split")
+    for n, t in (("b1", b1), ("w2", w2), ("b2", b2)):
         _need_contig(t, torch.float32, n)
     BT, H, W, C = x.shape
+    assert w1_split.shape == (64, 3, 3, C)
+    ws = torch.empty((BT, Ho, Wo, C), dtype=torch.float16, device=x.device)
     out = torch.empty((BT, Ho, Wo), dtype=torch.float32, device=x.device)
-    rc = _lib.lib().vda_depth_head(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
-                                   out.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
+    rc = _lib.lib().vda_depth_head(x.data_ptr(), w1_split.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                   out.data_ptr(), ws.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
     check(rc, "vda_depth_head")
     return out
