@@ -323,16 +323,33 @@ __device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
 }
 
-template <int BM, int BN, int NWM, int NWN, bool CONV, int ACT>
+template <int KB>
+__device__ __forceinline__ int swzk(int row, int chunk) {  // half offset in a [rows][KB] tile
+  constexpr int CH = KB / 8;
+  return row * KB + ((chunk ^ ((row >> 1) & (CH - 1))) << 3);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// NS-stage LDS-DMA pipeline: tile kt+NS-1 is issued while tile kt is multiplied; before reading a
+// stage every wave waits with a COUNTED vmcnt (its own newer pieces stay in flight) and passes a
+// raw s_barrier (no __syncthreads: its fence would drain every DMA in flight).
+template <int BM, int BN, int NWM, int NWN, int KB, int NS, bool CONV, int ACT>
 __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int NW = NWM * NWN;
   constexpr int WTM = BM / NWM, WTN = BN / NWN;  // wave tile
   constexpr int TM = WTM / 16, TN = WTN / 16;
   constexpr int ROWS = BM + BN;
-  constexpr int GROUPS = ROWS / 8;               // 1-KiB DMA pieces per tile
+  constexpr int CH = KB / 8;                     // 16-B chunks per row
+  constexpr int RPP = 64 / CH;                   // rows per 1-KiB DMA piece
+  constexpr int GROUPS = ROWS / RPP;             // pieces per stage
   static_assert(GROUPS % NW == 0, "pieces must divide evenly over the waves");
-  constexpr int IPW = GROUPS / NW;               // DMA instructions per wave per tile
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * ROWS * BK];
+  constexpr int IPW = GROUPS / NW;               // DMA instructions per wave per stage
+  constexpr int STAGE = ROWS * KB;               // halfs per stage
+  __shared__ __attribute__((aligned(1024))) h16 smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % NWM, wn = wave / NWM;
@@ -349,8 +366,8 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 #pragma unroll
   for (int i = 0; i < IPW; ++i) {
     const int g = wave * IPW + i;
-    const int R = g * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ ((R >> 1) & 7);
+    const int R = g * RPP + lane / CH;
+    const int c = (lane % CH) ^ ((R >> 1) & (CH - 1));
     kch[i] = c * 8;
     isx[i] = R < BM;
     if (R < BM) {
@@ -390,7 +407,7 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
           src = rowp[i] + k;
         }
       }
-      glds16(src, smem + buf * ROWS * BK + (wave * IPW + i) * 8 * BK);
+      glds16(src, smem + buf * STAGE + (wave * IPW + i) * RPP * KB);
     }
   };
 
@@ -400,25 +417,42 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
-  issue(0, 0);
-  __syncthreads();
+  const int nk = (p.K + KB - 1) / KB;
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s * KB, s);
   const int frow = lane & 15, fchunk = lane >> 4;
   const bool prerelu = CONV && p.pre_relu;
+  int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) issue((kt + 1) * BK, buf ^ 1);
-    const h16* sX = smem + buf * ROWS * BK;
-    const h16* sW = sX + BM * BK;
+    // tile kt must have landed; the (up to NS-2) newer tiles may stay in flight
+    const int newer = min(NS - 2, nk - 1 - kt);
+    if constexpr (NS >= 4) {
+      if (newer >= 2) wait_vmcnt<2 * IPW>();
+      else if (newer == 1) wait_vmcnt<IPW>();
+      else wait_vmcnt<0>();
+    } else if constexpr (NS == 3) {
+      if (newer >= 1) wait_vmcnt<IPW>();
+      else wait_vmcnt<0>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    {
+      const int nxt = kt + NS - 1;
+      if (nxt < nk) issue(nxt * KB, nxt % NS);
+    }
+    const h16* sX = smem + buf * STAGE;
+    const h16* sW = sX + BM * KB;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KB / 32; ++ks) {
       h8 af[TN], bf[TM];
 #pragma unroll
       for (int i = 0; i < TN; ++i)
-        af[i] = *reinterpret_cast<const h8*>(&sW[swz(wn * WTN + i * 16 + frow, ks * 4 + fchunk)]);
+        af[i] = *reinterpret_cast<const h8*>(&sW[swzk<KB>(wn * WTN + i * 16 + frow, ks * 4 + fchunk)]);
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
-        bf[j] = *reinterpret_cast<const h8*>(&sX[swz(wm * WTM + j * 16 + frow, ks * 4 + fchunk)]);
+        bf[j] = *reinterpret_cast<const h8*>(&sX[swzk<KB>(wm * WTM + j * 16 + frow, ks * 4 + fchunk)]);
         if (prerelu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) bf[j][e] = bf[j][e] > (h16)0 ? bf[j][e] : (h16)0;
@@ -429,7 +463,7 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 #pragma unroll
         for (int j = 0; j < TM; ++j) acc[i][j] = mfma16(af[i], bf[j], acc[i][j]);
     }
-    __syncthreads();
+    buf = (buf + 1 == NS) ? 0 : buf + 1;
   }
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
@@ -484,13 +518,296 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
   }
 }
 
+// ---- 256x256 phased kernel -------------------------------------------------------------------
+// 8 waves (2 m x 4 n), wave tile 128 (m) x 64 (n), BK = 64, two K-tile buffers of four 16-KiB
+// half-tile regions [XL | XH | WL | WH].  Every K tile runs as 4 phases; each phase multiplies one
+// 64 x 32 quadrant of the wave tile (16 MFMAs) between two barriers, loading the fragments it needs
+// (quadrant order (0,0) (0,1) (1,1) (1,0) reuses the previous phase's X or W fragments):
+//   P1: ds_read X(q0) + W(q0); DMA XL, XH of tile t+1 | P2: ds_read W(q1); DMA WL, WH of tile t+1
+//   P3: ds_read X(q1)                                 | P4: ds_read W(q0); s_waitcnt vmcnt(0)
+// Waves 4-7 run one barrier behind waves 0-3, so the two waves sharing a SIMD alternate between
+// their LDS-read segment and their MFMA segment.  Restaging a region is >= 2 phases after its
+// last read and the DMA wait is one phase before the first read of the new tile (the margins the
+// stagger needs).  Raw s_barrier + explicit waits only: nothing drains the DMA queue implicitly.
+template <bool CONV, int ACT>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n) {
+  constexpr int HALF = 128 * BK;            // halfs per half-tile region (16 KiB)
+  constexpr int BUF = 4 * HALF;             // one K tile
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  int tile_m, tile_n;
+  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, tile_m, tile_n);
+  const int m0 = tile_m * 256, n0 = tile_n * 256;
+
+  // this lane's DMA rows: pieces 2*wave and 2*wave+1 of every half-tile region
+  const h16* xrow[2][2];
+  const h16* wrow[2][2];
+  bool xok[2][2], wok[2][2];
+  int kch[2];
+  int cbt[2][2], coy[2][2], cox[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = (2 * wave + i) * 8 + (lane >> 3);
+    kch[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int m = m0 + hh * 128 + r;
+      xok[hh][i] = m < p.M;
+      const int mm = xok[hh][i] ? m : 0;
+      if constexpr (CONV) {
+        cox[hh][i] = mm % p.Wo;
+        const int t = mm / p.Wo;
+        coy[hh][i] = t % p.Ho;
+        cbt[hh][i] = t / p.Ho;
+        xrow[hh][i] = p.x;
+      } else {
+        xrow[hh][i] = p.x + (long)mm * p.ldx;
+      }
+      const int n = n0 + hh * 128 + r;
+      wok[hh][i] = n < p.N;
+      wrow[hh][i] = p.w + (long)(wok[hh][i] ? n : 0) * p.K;
+    }
+  }
+  const void* zero = (const void*)g_zero_page;
+  auto dma_x = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = k0 + kch[i];
+        const void* src = zero;
+        if (xok[hh][i] && k < p.K) {
+          if constexpr (CONV) {
+            const int tap = k / p.Cin, ci = k - tap * p.Cin;
+            const int ky = tap / p.ks, kx = tap - ky * p.ks;
+            const int iy = coy[hh][i] * p.stride - p.pad + ky, ix = cox[hh][i] * p.stride - p.pad + kx;
+            if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+              src = p.x + (((long)cbt[hh][i] * p.H + iy) * p.W + ix) * p.Cin + ci;
+          } else {
+            src = xrow[hh][i] + k;
+          }
+        }
+        glds16(src, smem + buf * BUF + hh * HALF + (2 * wave + i) * 8 * BK);
+      }
+  };
+  auto dma_w = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int k = k0 + kch[i];
+        const void* src = (wok[hh][i] && k < p.K) ? (const void*)(wrow[hh][i] + k) : zero;
+        glds16(src, smem + buf * BUF + (2 + hh) * HALF + (2 * wave + i) * 8 * BK);
+      }
+  };
+
+  f4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  const int frow = lane & 15, fchunk = lane >> 4;
+  const bool prerelu = CONV && p.pre_relu;
+  // wave's regions: X half wm (rows 0..127 of it), W half wn>>1 at row offset (wn&1)*64
+  const int xoff = wm * HALF;
+  const int woff = 2 * HALF + (wn >> 1) * HALF;
+  const int wrow0 = (wn & 1) * 64;
+
+  dma_x(0, 0);
+  dma_w(0, 0);
+  wait_vmcnt<0>();
+  __builtin_amdgcn_s_barrier();
+  const bool lagging = wave >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();  // stagger waves 4-7 by one barrier
+
+  h8 xf[4][2], wf[2][2];
+  auto load_x = [&](const h16* base, int qm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        xf[j][ks] = *reinterpret_cast<const h8*>(&base[xoff + swz(qm * 64 + j * 16 + frow, ks * 4 + fchunk)]);
+        if (prerelu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[j][ks][e] = xf[j][ks][e] > (h16)0 ? xf[j][ks][e] : (h16)0;
+        }
+      }
+  };
+  auto load_w = [&](const h16* base, int qn) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        wf[i][ks] = *reinterpret_cast<const h8*>(&base[woff + swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
+  };
+  auto mma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[qn * 2 + i][qm * 4 + j] = mfma16(wf[i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const h16* base = smem + (kt & 1) * BUF;
+    const int nb = (kt + 1) & 1;
+    const bool more = kt + 1 < nk;
+    // P1
+    load_x(base, 0);
+    load_w(base, 0);
+    if (more) dma_x(kt + 1, nb);
+    mma(0, 0);
+    // P2
+    load_w(base, 1);
+    if (more) dma_w(kt + 1, nb);
+    mma(0, 1);
+    // P3
+    load_x(base, 1);
+    mma(1, 1);
+    // P4
+    load_w(base, 0);
+    wait_vmcnt<0>();
+    mma(1, 0);
+  }
+  if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
+
+  const int mcol = lane & 15, nq = (lane >> 4) * 4;
+  if (p.epi.store == VDA_STORE_ROWS) {
+    // LDS-staged epilogue: phase 1 writes t = gamma * act(acc + bias + rowbias) as fp16 into a
+    // [256][OW] image (8-byte units XOR-swizzled by row&15: conflict-free both ways); phase 2 reads
+    // it back as whole rows, adds the residual(s) with 16-byte loads and stores 16-byte chunks, so
+    // every output row is written by full contiguous 128-B lines.
+    constexpr int OW = (ACT == VDA_ACT_GEGLU) ? 128 : 256;  // output columns of this tile
+    constexpr int UPR = OW / 4;                              // 8-byte units per row
+    __syncthreads();                                         // all waves done with the operand image
+    const vda_epilogue& e = p.epi;
+#pragma unroll
+    for (int i = 0; i < 4; i += (ACT == VDA_ACT_GEGLU ? 2 : 1)) {
+      const int nl = wn * 64 + i * 16 + nq;  // local W row of this lane's first channel
+      const int n = n0 + nl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ml = wm * 128 + j * 16 + mcol;
+        const int m = m0 + ml;
+        f4 v;
+        int col;
+        if constexpr (ACT == VDA_ACT_GEGLU) {
+          f4 vh = acc[i][j], vg = acc[i + 1][j];
+          if (e.bias && n < p.N) {
+            vh += *reinterpret_cast<const f4*>(e.bias + n);
+            vg += *reinterpret_cast<const f4*>(e.bias + n + 16);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = vh[r] * gelu_erf(vg[r]);
+          col = ((wn * 64 + i * 16) >> 1) + nq;
+          if (e.gamma && n < p.N) v *= *reinterpret_cast<const f4*>(e.gamma + (n0 >> 1) + col);
+        } else {
+          v = acc[i][j];
+          if (n < p.N) {
+            if (e.bias) v += *reinterpret_cast<const f4*>(e.bias + n);
+            if (e.rowbias && m < p.M) v += *reinterpret_cast<const f4*>(e.rowbias + (long)((m / e.rdiv) % e.rmod) * p.N + n);
+          }
+          if constexpr (ACT == VDA_ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+          } else if constexpr (ACT == VDA_ACT_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+          }
+          if (e.gamma && n < p.N) v *= *reinterpret_cast<const f4*>(e.gamma + n);
+          col = nl;
+        }
+        h4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (h16)v[r];
+        const int u = (col >> 2) ^ (ml & 15);
+        *reinterpret_cast<h4*>(&smem[ml * OW + u * 4]) = o;
+      }
+    }
+    __syncthreads();
+    const int nout = (ACT == VDA_ACT_GEGLU) ? (p.N >> 1) : p.N;
+    const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
+    constexpr int CPR = OW / 8;  // 16-byte chunks per row
+#pragma unroll 4
+    for (int idx = tid; idx < 256 * CPR; idx += 512) {
+      const int row = idx / CPR, q = idx - row * CPR;
+      const int m = m0 + row;
+      const int c = cout0 + q * 8;
+      if (m >= p.M || c >= nout) continue;
+      const int s = row & 15;
+      const uint4 raw = *reinterpret_cast<const uint4*>(&smem[row * OW + ((2 * q) ^ (s & ~1)) * 4]);
+      h8 t = __builtin_bit_cast(h8, (s & 1) ? make_uint4(raw.z, raw.w, raw.x, raw.y) : raw);
+      if (e.res || e.res2) {
+        float f[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) f[r] = (float)t[r];
+        if (e.res) {
+          const h8 a = __builtin_bit_cast(h8, ldg16((const h16*)e.res + (long)m * e.ldres + c));
+#pragma unroll
+          for (int r = 0; r < 8; ++r) f[r] += (float)a[r];
+        }
+        if (e.res2) {
+          const h8 a = __builtin_bit_cast(h8, ldg16((const h16*)e.res2 + (long)m * e.ldres2 + c));
+#pragma unroll
+          for (int r = 0; r < 8; ++r) f[r] += (float)a[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) t[r] = (h16)f[r];
+      }
+      stg16(p.y + (long)m * p.ldy + c, __builtin_bit_cast(uint4, t));
+    }
+    return;
+  }
+  if constexpr (ACT == VDA_ACT_GEGLU) {
+
+#pragma unroll
+    for (int i = 0; i < 4; i += 2) {
+      const int nbase = n0 + wn * 64 + i * 16;
+      if (nbase >= p.N) continue;
+      const int n_out = (nbase >> 1) + nq;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + wm * 128 + j * 16 + mcol;
+        if (m < p.M) epi_geglu4(p, m, nbase + nq, nbase + 16 + nq, n_out, acc[i][j], acc[i + 1][j]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + nq;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + wm * 128 + j * 16 + mcol;
+        if (m < p.M) epi_store4<ACT>(p, m, n, acc[i][j]);
+      }
+    }
+  }
+}
+
 int g_force_tile = -1;  // debug / tuning override (vda_debug_force_tile)
 
-template <int BM, int BN, int NWM, int NWN, bool CONV, int ACT>
+template <int BM, int BN, int NWM, int NWN, int KB, int NS, bool CONV, int ACT>
 void launch_tile(const GemmParams& p, hipStream_t st) {
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, NWM, NWN, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(NWM * NWN * 64), 0, st,
-                     p, tiles_m, tiles_n);
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, NWM, NWN, KB, NS, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(NWM * NWN * 64),
+                     0, st, p, tiles_m, tiles_n);
 }
 
 template <bool CONV, int ACT>
@@ -499,16 +816,27 @@ void launch_act(const GemmParams& p, hipStream_t st) {
   if (cfg < 0) {
     // measured on MI355X (tools/bench_gemm.py): 256x256 wins every large-N shape; N = 128 prefers
     // 256x128; short K (<= 256) and narrow N prefer the 2-blocks-per-CU 128x64 tile.
+    const vda_epilogue& e = p.epi;
+    const bool a16 = ((uintptr_t)p.y % 16 == 0) && p.ldy % 8 == 0 && p.N % 8 == 0 &&
+                     (!e.res || ((uintptr_t)e.res % 16 == 0 && e.ldres % 8 == 0)) &&
+                     (!e.res2 || ((uintptr_t)e.res2 % 16 == 0 && e.ldres2 % 8 == 0)) &&
+                     (e.act != VDA_ACT_GEGLU || (p.N / 2) % 8 == 0);
     if (p.N <= 64 || p.K <= 256) cfg = 2;
+    else if (!CONV && p.N >= 256 && p.M >= 4096 && a16 && e.store == VDA_STORE_ROWS) cfg = 4;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
     else cfg = 0;
   }
   switch (cfg) {
-    case 1: launch_tile<256, 128, 4, 2, CONV, ACT>(p, st); break;
-    case 2: launch_tile<128, 64, 2, 2, CONV, ACT>(p, st); break;
-    case 3: launch_tile<256, 256, 2, 4, CONV, ACT>(p, st); break;
-    default: launch_tile<128, 128, 2, 2, CONV, ACT>(p, st); break;
+    case 1: launch_tile<256, 128, 4, 2, 32, 4, CONV, ACT>(p, st); break;
+    case 2: launch_tile<128, 64, 2, 2, 32, 4, CONV, ACT>(p, st); break;
+    case 3: launch_tile<256, 256, 2, 4, 32, 4, CONV, ACT>(p, st); break;
+    case 4: {
+      const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
+      hipLaunchKernelGGL((gemm256_kernel<CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
+      break;
+    }
+    default: launch_tile<128, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
   }
 }
 
@@ -631,7 +959,7 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   p.epi = default_epi();
   p.epi.bias = b1; p.epi.gamma = w2; p.epi.rowbias = b2;
   const int tiles_m = (p.M + 127) / 128;
-  hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, true, ACT_DEPTH>), dim3(tiles_m), dim3(256), 0, st, p, tiles_m, 1);
+  hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, 32, 4, true, ACT_DEPTH>), dim3(tiles_m), dim3(256), 0, st, p, tiles_m, 1);
   VDA_LAUNCH_CHECK();
   return 0;
 }
