@@ -6,7 +6,7 @@ ARCH    ?= gfx950
 PKG     := video-depth-anything_amd
 SRCS    := $(wildcard $(PKG)/csrc/*.hip)
 OBJS    := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(SRCS))
-CXXFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -I include -munsafe-fp-atomics
+CXXFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -I include -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form
 
 all: $(PKG)/libvda.so
 

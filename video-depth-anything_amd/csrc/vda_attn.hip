@@ -1,6 +1,7 @@
 // Spatial (DINOv2) and temporal (motion-module) attention, fp16 MFMA + fp32 online softmax.
 #include "vda_common.h"
 #include "../../include/vda.h"
+#include <type_traits>
 
 namespace {
 
@@ -35,15 +36,19 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
   const h16* base = qkv + (long)b * N * ld;
   const int g = lane >> 4, li = lane & 15;
 
-  // Q fragments: B operand, lane holds Q[q = qs*16 + li][d = ks*32 + 8g .. +7]
+  // Q fragments (B operand), pre-scaled by scale*log2(e) so scores come out in log2 units:
+  // lane holds Q[q = qs*16 + li][d = ks*32 + 8g .. +7]
   h8 qf[2][2];
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
     const int q = blockIdx.x * SQB + wave * 32 + qs * 16 + li;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      if (q < N) qf[qs][ks] = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + h * SD + ks * 32 + g * 8));
-      else qf[qs][ks] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      h8 t = h8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (q < N) t = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + h * SD + ks * 32 + g * 8));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (h16)((float)t[e] * scale_log2);
+      qf[qs][ks] = t;
     }
   }
 
@@ -79,15 +84,11 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
     }
   };
 
-  const int ntiles = (N + SKB - 1) / SKB;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // one 64-key tile; MASK only for the last (partial) tile
+  auto tile = [&](int kt, auto mask_tag) {
+    constexpr bool MASK = decltype(mask_tag)::value;
     const int buf = kt & 1;
-    if (kt + 1 < ntiles) gload(kt + 1);
-
-    // ---- Sᵀ = K Qᵀ : s[kt4][qs] lane holds keys kt4*16 + 4g + r, query qs*16 + li
+    // ---- Sᵀ = K Qᵀ : s[a][qs] lane holds keys a*16 + 4g + r, query qs*16 + li
     f4 s[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -102,47 +103,51 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
         for (int qs = 0; qs < 2; ++qs) s[a][qs] = mfma16(kf, qf[qs][ks], s[a][qs]);
       }
     }
-    // ---- online softmax (base-2), mask keys >= N
-    const int kbase = kt * SKB;
-    const bool tail = kbase + SKB > N;
-    h8 pf[2][2];  // [qs][kc] P fragments (B operand of PV)
-#pragma unroll
-    for (int qs = 0; qs < 2; ++qs) {
-      float mx = -INFINITY;
+    if constexpr (MASK) {
+      const int kbase = kt * SKB;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = s[a][qs][r] * scale_log2;
-          if (tail && kbase + a * 16 + 4 * g + r >= N) t = -INFINITY;
-          s[a][qs][r] = t;
-          mx = fmaxf(mx, t);
-        }
+        for (int r = 0; r < 4; ++r)
+          if (kbase + a * 16 + 4 * g + r >= N) { s[a][0][r] = -INFINITY; s[a][1][r] = -INFINITY; }
+    }
+    // ---- online softmax (base 2); the O/l rescale is skipped when no row max grew (wave vote)
+    h8 pf[2][2];  // [qs][kc] P fragments (B operand of PV)
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      float mx = fmaxf(fmaxf(fmaxf(s[0][qs][0], s[0][qs][1]), fmaxf(s[0][qs][2], s[0][qs][3])),
+                       fmaxf(fmaxf(s[1][qs][0], s[1][qs][1]), fmaxf(s[1][qs][2], s[1][qs][3])));
+      mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(s[2][qs][0], s[2][qs][1]), fmaxf(s[2][qs][2], s[2][qs][3])),
+                           fmaxf(fmaxf(s[3][qs][0], s[3][qs][1]), fmaxf(s[3][qs][2], s[3][qs][3]))));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(mrun[qs], mx);
-      const float alpha = exp2f(mrun[qs] - mnew);
-      mrun[qs] = mnew;
+      if (__any(mx > mrun[qs])) {
+        const float mnew = fmaxf(mrun[qs], mx);
+        const float alpha = __builtin_amdgcn_exp2f(mrun[qs] - mnew);
+        mrun[qs] = mnew;
+        lrun[qs] *= alpha;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) o[d][qs] *= alpha;
+      }
+      const float m = mrun[qs];
       float ps = 0.f;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = exp2f(s[a][qs][r] - mnew);
+          const float pv = __builtin_amdgcn_exp2f(s[a][qs][r] - m);
           ps += pv;
           pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)pv;
         }
-      lrun[qs] = lrun[qs] * alpha + ps;
-#pragma unroll
-      for (int d = 0; d < 4; ++d) o[d][qs] *= alpha;
+      lrun[qs] += ps;
     }
     // ---- Oᵀ += Vᵀ Pᵀ
+    const int q4 = li >> 2, p4 = li & 3;
 #pragma unroll
     for (int kc = 0; kc < 2; ++kc) {
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
         // lane 4q+p of group g: row kc*32 + 4g + q, cols d*16 + 4p
-        const int q4 = li >> 2, p4 = li & 3;
         const int col = d * 16 + 4 * p4;
         const int r0 = kc * 32 + 4 * g + q4, r1 = r0 + 16;
         const h4 v0 = lds_read_tr16(&sV[buf][v_swz(r0, col >> 3) + (col & 7)]);
@@ -152,7 +157,18 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
         for (int qs = 0; qs < 2; ++qs) o[d][qs] = mfma16(vf, pf[qs][kc], o[d][qs]);
       }
     }
-    if (kt + 1 < ntiles) sstore(buf ^ 1);
+  };
+
+  const int ntiles = (N + SKB - 1) / SKB;
+  const int nfull = N / SKB;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    if (kt + 1 < ntiles) gload(kt + 1);
+    if (kt < nfull) tile(kt, std::false_type{});
+    else tile(kt, std::true_type{});
+    if (kt + 1 < ntiles) sstore((kt + 1) & 1);
     __syncthreads();
   }
   // ---- epilogue: normalise and store (lane: d = dsub*16 + 4g + r, q = qs*16 + li)
