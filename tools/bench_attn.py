@@ -11,7 +11,7 @@ def t(fn, n=10):
     e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1) / n
 B, N, H, D = 32, 1370, 16, 64
-qkv = torch.randn(B * N, 3 * H * D, device="cuda", dtype=torch.float16)
+qkv = (torch.randn(B * N, 3 * H * D, device="cuda") * 0.5).half()  # NB: in-situ timings (rocprof of bench.py) are the ground truth
 ms = t(lambda: ops.spatial_attention(qkv, B, N, H, D))
 print(f"spatial B={B} N={N} H={H}: {ms*1e3:.1f} us  {4*B*H*N*N*D/ms/1e9:.1f} TFLOP/s", flush=True)
 for (S, C) in [(1369, 1024), (361, 1024), (1369, 256), (5476, 256)]:

@@ -1,7 +1,7 @@
 """Print per-kernel register / LDS / occupancy from hipcc -Rpass-analysis=kernel-resource-usage."""
 import re, subprocess, sys
 src = sys.argv[1]
-out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", "include", "-c", src,
+out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-I", "include", "-mllvm", "-amdgpu-mfma-vgpr-form", "-c", src,
                       "-o", "/tmp/_kres.o", "-Rpass-analysis=kernel-resource-usage"], capture_output=True, text=True).stderr
 cur = None; rows = []
 for line in out.splitlines():

@@ -11,7 +11,7 @@ import os
 from ctypes import c_float, c_int32, c_int64, c_void_p, POINTER
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvda.so")
+LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so")  # override: tuning experiments only
 
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
