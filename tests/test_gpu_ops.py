@@ -90,10 +90,12 @@ def test_conv_transpose_pixel_shuffle(k, cin, cout):
     assert rel(y, ref) < 2e-3
 
 
-@pytest.mark.parametrize("cin,cout,stride,H,W", [(64, 64, 1, 9, 11), (48, 64, 1, 12, 12), (256, 256, 1, 19, 19),
-                                                 (384, 384, 2, 9, 9), (1024, 256, 1, 5, 5), (96, 32, 1, 3, 4)])
-def test_conv3x3(cin, cout, stride, H, W):
-    BT = 2
+@pytest.mark.parametrize("cin,cout,stride,H,W,BT", [(64, 64, 1, 9, 11, 2), (48, 64, 1, 12, 12, 2), (256, 256, 1, 19, 19, 2),
+                                                    (384, 384, 2, 9, 9, 2), (1024, 256, 1, 5, 5, 2), (96, 32, 1, 3, 4, 2),
+                                                    # large M: the phased 256x256 kernel (uniform-tap / general loaders)
+                                                    (256, 256, 1, 40, 40, 4), (48, 256, 1, 40, 40, 4),
+                                                    (512, 256, 2, 60, 60, 8)])
+def test_conv3x3(cin, cout, stride, H, W, BT):
     x = rnd(BT, cin, H, W, seed=18)
     w = rnd(cout, cin, 3, 3, scale=(9 * cin) ** -0.5, seed=19)
     b = rnd(cout, scale=0.1, seed=20)

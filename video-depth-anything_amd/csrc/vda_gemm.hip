@@ -562,7 +562,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
         const int t = mm / p.Wo;
         coy[hh][i] = t % p.Ho;
         cbt[hh][i] = t / p.Ho;
-        xrow[hh][i] = p.x;
+        coy[hh][i] = coy[hh][i] * p.stride - p.pad;  // top-left input row / col of the window
+        cox[hh][i] = cox[hh][i] * p.stride - p.pad;
+        xrow[hh][i] = p.x + (((long)cbt[hh][i] * p.H + coy[hh][i]) * p.W + cox[hh][i]) * p.Cin;
       } else {
         xrow[hh][i] = p.x + (long)mm * p.ldx;
       }
@@ -572,8 +574,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     }
   }
   const void* zero = (const void*)g_zero_page;
+  // conv: when Cin % 64 == 0 a K tile never straddles a tap, so the tap is wave-uniform (scalar
+  // math) and a lane only adds a scalar offset to its window base; otherwise per-lane division.
+  const bool tap_uniform = CONV && (p.Cin % BK == 0);
   auto dma_x = [&](int kt, int buf) {
     const int k0 = kt * BK;
+    int ky = 0, kx = 0, ci0 = 0;
+    long toff = 0;
+    if (tap_uniform) {
+      const int tap = k0 / p.Cin;
+      ci0 = k0 - tap * p.Cin;
+      ky = tap / p.ks;
+      kx = tap - ky * p.ks;
+      toff = ((long)ky * p.W + kx) * p.Cin + ci0;
+    }
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
@@ -582,11 +596,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
         const void* src = zero;
         if (xok[hh][i] && k < p.K) {
           if constexpr (CONV) {
-            const int tap = k / p.Cin, ci = k - tap * p.Cin;
-            const int ky = tap / p.ks, kx = tap - ky * p.ks;
-            const int iy = coy[hh][i] * p.stride - p.pad + ky, ix = cox[hh][i] * p.stride - p.pad + kx;
-            if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-              src = p.x + (((long)cbt[hh][i] * p.H + iy) * p.W + ix) * p.Cin + ci;
+            if (tap_uniform) {
+              if ((unsigned)(coy[hh][i] + ky) < (unsigned)p.H && (unsigned)(cox[hh][i] + kx) < (unsigned)p.W)
+                src = xrow[hh][i] + toff + kch[i];
+            } else {
+              const int tap = k / p.Cin, ci = k - tap * p.Cin;
+              const int ty = tap / p.ks, tx = tap - ty * p.ks;
+              const int iy = coy[hh][i] + ty, ix = cox[hh][i] + tx;
+              if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+                src = p.x + (((long)cbt[hh][i] * p.H + iy) * p.W + ix) * p.Cin + ci;
+            }
           } else {
             src = xrow[hh][i] + k;
           }
@@ -822,7 +841,7 @@ void launch_act(const GemmParams& p, hipStream_t st) {
                      (!e.res2 || ((uintptr_t)e.res2 % 16 == 0 && e.ldres2 % 8 == 0)) &&
                      (e.act != VDA_ACT_GEGLU || (p.N / 2) % 8 == 0);
     if (p.N <= 64 || p.K <= 256) cfg = 2;
-    else if (!CONV && p.N >= 256 && p.M >= 4096 && a16 && e.store == VDA_STORE_ROWS) cfg = 4;
+    else if (p.N >= 256 && p.M >= 4096 && a16 && e.store == VDA_STORE_ROWS) cfg = 4;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
     else cfg = 0;
