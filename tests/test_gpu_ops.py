@@ -94,7 +94,7 @@ def test_conv_transpose_pixel_shuffle(k, cin, cout):
                                                     (384, 384, 2, 9, 9, 2), (1024, 256, 1, 5, 5, 2), (96, 32, 1, 3, 4, 2),
                                                     # large M: the phased 256x256 kernel (uniform-tap / general loaders)
                                                     (256, 256, 1, 40, 40, 4), (48, 256, 1, 40, 40, 4),
-                                                    (512, 256, 2, 60, 60, 8)])
+                                                    (512, 256, 2, 60, 60, 8), (256, 128, 1, 60, 60, 4)])
 def test_conv3x3(cin, cout, stride, H, W, BT):
     x = rnd(BT, cin, H, W, seed=18)
     w = rnd(cout, cin, 3, 3, scale=(9 * cin) ** -0.5, seed=19)

@@ -529,45 +529,50 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 // their LDS-read segment and their MFMA segment.  Restaging a region is >= 2 phases after its
 // last read and the DMA wait is one phase before the first read of the new tile (the margins the
 // stagger needs).  Raw s_barrier + explicit waits only: nothing drains the DMA queue implicitly.
-template <bool CONV, int ACT>
+template <int XR, int WR, bool CONV, int ACT>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
 __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n) {
-  constexpr int HALF = 128 * BK;            // halfs per half-tile region (16 KiB)
-  constexpr int BUF = 4 * HALF;             // one K tile
+  static_assert(XR * WR == 4 && (XR == 2 || XR == 4), "8 waves as XR (m) x 8/XR (n), wave tile 128 x 64");
+  constexpr int BM = 128 * XR, BN = 128 * WR;
+  constexpr int HALF = 128 * BK;            // halfs per 128-row region (16 KiB)
+  constexpr int BUF = (XR + WR) * HALF;     // one K tile
   __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
+  const int wm = wave % XR, wn = wave / XR;
   int tile_m, tile_n;
   tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, tile_m, tile_n);
-  const int m0 = tile_m * 256, n0 = tile_n * 256;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
 
   // this lane's DMA rows: pieces 2*wave and 2*wave+1 of every half-tile region
-  const h16* xrow[2][2];
-  const h16* wrow[2][2];
-  bool xok[2][2], wok[2][2];
+  const h16* xrow[XR][2];
+  const h16* wrow[WR][2];
+  bool xok[XR][2], wok[WR][2];
   int kch[2];
-  int cbt[2][2], coy[2][2], cox[2][2];
+  int cyx[XR][2];  // conv: top-left input (row << 16 | col & 0xffff) of the output pixel's window
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int r = (2 * wave + i) * 8 + (lane >> 3);
     kch[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < XR; ++hh) {
       const int m = m0 + hh * 128 + r;
       xok[hh][i] = m < p.M;
       const int mm = xok[hh][i] ? m : 0;
       if constexpr (CONV) {
-        cox[hh][i] = mm % p.Wo;
+        const int ox = mm % p.Wo;
         const int t = mm / p.Wo;
-        coy[hh][i] = t % p.Ho;
-        cbt[hh][i] = t / p.Ho;
-        coy[hh][i] = coy[hh][i] * p.stride - p.pad;  // top-left input row / col of the window
-        cox[hh][i] = cox[hh][i] * p.stride - p.pad;
-        xrow[hh][i] = p.x + (((long)cbt[hh][i] * p.H + coy[hh][i]) * p.W + cox[hh][i]) * p.Cin;
+        const int oy = t % p.Ho, bt = t / p.Ho;
+        const int iy0 = xok[hh][i] ? oy * p.stride - p.pad : -32768;  // invalid rows fail every bound
+        const int ix0 = ox * p.stride - p.pad;
+        cyx[hh][i] = (iy0 << 16) | (ix0 & 0xffff);
+        xrow[hh][i] = p.x + (((long)bt * p.H + oy * p.stride - p.pad) * p.W + ix0) * p.Cin;
       } else {
         xrow[hh][i] = p.x + (long)mm * p.ldx;
       }
+    }
+#pragma unroll
+    for (int hh = 0; hh < WR; ++hh) {
       const int n = n0 + hh * 128 + r;
       wok[hh][i] = n < p.N;
       wrow[hh][i] = p.w + (long)(wok[hh][i] ? n : 0) * p.K;
@@ -589,26 +594,27 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
       toff = ((long)ky * p.W + kx) * p.Cin + ci0;
     }
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < XR; ++hh)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int k = k0 + kch[i];
         const void* src = zero;
-        if (xok[hh][i] && k < p.K) {
-          if constexpr (CONV) {
+        if constexpr (CONV) {
+          if (k < p.K) {
             if (tap_uniform) {
-              if ((unsigned)(coy[hh][i] + ky) < (unsigned)p.H && (unsigned)(cox[hh][i] + kx) < (unsigned)p.W)
+              if ((unsigned)((cyx[hh][i] >> 16) + ky) < (unsigned)p.H &&
+                  (unsigned)((short)(cyx[hh][i] & 0xffff) + kx) < (unsigned)p.W)
                 src = xrow[hh][i] + toff + kch[i];
             } else {
               const int tap = k / p.Cin, ci = k - tap * p.Cin;
               const int ty = tap / p.ks, tx = tap - ty * p.ks;
-              const int iy = coy[hh][i] + ty, ix = cox[hh][i] + tx;
-              if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-                src = p.x + (((long)cbt[hh][i] * p.H + iy) * p.W + ix) * p.Cin + ci;
+              if ((unsigned)((cyx[hh][i] >> 16) + ty) < (unsigned)p.H &&
+                  (unsigned)((short)(cyx[hh][i] & 0xffff) + tx) < (unsigned)p.W)
+                src = xrow[hh][i] + ((long)ty * p.W + tx) * p.Cin + ci;
             }
-          } else {
-            src = xrow[hh][i] + k;
           }
+        } else if (xok[hh][i] && k < p.K) {
+          src = xrow[hh][i] + k;
         }
         glds16(src, smem + buf * BUF + hh * HALF + (2 * wave + i) * 8 * BK);
       }
@@ -616,12 +622,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   auto dma_w = [&](int kt, int buf) {
     const int k0 = kt * BK;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < WR; ++hh)
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int k = k0 + kch[i];
         const void* src = (wok[hh][i] && k < p.K) ? (const void*)(wrow[hh][i] + k) : zero;
-        glds16(src, smem + buf * BUF + (2 + hh) * HALF + (2 * wave + i) * 8 * BK);
+        glds16(src, smem + buf * BUF + (XR + hh) * HALF + (2 * wave + i) * 8 * BK);
       }
   };
 
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   const bool prerelu = CONV && p.pre_relu;
   // wave's regions: X half wm (rows 0..127 of it), W half wn>>1 at row offset (wn&1)*64
   const int xoff = wm * HALF;
-  const int woff = 2 * HALF + (wn >> 1) * HALF;
+  const int woff = XR * HALF + (wn >> 1) * HALF;
   const int wrow0 = (wn & 1) * 64;
 
   dma_x(0, 0);
@@ -712,7 +718,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     // [256][OW] image (8-byte units XOR-swizzled by row&15: conflict-free both ways); phase 2 reads
     // it back as whole rows, adds the residual(s) with 16-byte loads and stores 16-byte chunks, so
     // every output row is written by full contiguous 128-B lines.
-    constexpr int OW = (ACT == VDA_ACT_GEGLU) ? 128 : 256;  // output columns of this tile
+    constexpr int OW = (ACT == VDA_ACT_GEGLU) ? BN / 2 : BN;  // output columns of this tile
     constexpr int UPR = OW / 4;                              // 8-byte units per row
     __syncthreads();                                         // all waves done with the operand image
     const vda_epilogue& e = p.epi;
@@ -764,7 +770,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
     constexpr int CPR = OW / 8;  // 16-byte chunks per row
 #pragma unroll 4
-    for (int idx = tid; idx < 256 * CPR; idx += 512) {
+    for (int idx = tid; idx < BM * CPR; idx += 512) {
       const int row = idx / CPR, q = idx - row * CPR;
       const int m = m0 + row;
       const int c = cout0 + q * 8;
@@ -842,6 +848,7 @@ void launch_act(const GemmParams& p, hipStream_t st) {
                      (e.act != VDA_ACT_GEGLU || (p.N / 2) % 8 == 0);
     if (p.N <= 64 || p.K <= 256) cfg = 2;
     else if (p.N >= 256 && p.M >= 4096 && a16 && e.store == VDA_STORE_ROWS) cfg = 4;
+    else if (p.N == 128 && p.M >= 8192 && a16 && e.store == VDA_STORE_ROWS) cfg = 5;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
     else cfg = 0;
@@ -852,7 +859,12 @@ void launch_act(const GemmParams& p, hipStream_t st) {
     case 3: launch_tile<256, 256, 2, 4, 32, 4, CONV, ACT>(p, st); break;
     case 4: {
       const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-      hipLaunchKernelGGL((gemm256_kernel<CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
+      hipLaunchKernelGGL((gemm256_kernel<2, 2, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
+      break;
+    }
+    case 5: {
+      const int tiles_m = (p.M + 511) / 512, tiles_n = (p.N + 127) / 128;
+      hipLaunchKernelGGL((gemm256_kernel<4, 1, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
       break;
     }
     default: launch_tile<128, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
