@@ -630,6 +630,45 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
         glds16(src, smem + buf * BUF + (XR + hh) * HALF + (2 * wave + i) * 8 * BK);
       }
   };
+  // Dense GEMMs (K % 64 == 0, operands < 4 GiB): buffer_load ... lds with a per-lane byte offset
+  // that never changes (row, chunk) and the K advance in the scalar soffset, so issuing a piece
+  // costs no VALU at all; rows >= M / N get an offset past num_records and read zeros.
+  __amdgpu_buffer_rsrc_t xrs, wrs;
+  unsigned xvo[XR][2], wvo[WR][2];
+  if constexpr (!CONV) {
+    xrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(unsigned)((long)p.M * p.ldx * 2), 0x00020000);
+    wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)(unsigned)((long)p.N * p.K * 2), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (2 * wave + i) * 8 + (lane >> 3);
+#pragma unroll
+      for (int hh = 0; hh < XR; ++hh) {
+        const int m = m0 + hh * 128 + r;
+        xvo[hh][i] = m < p.M ? (unsigned)(((long)m * p.ldx + kch[i]) * 2) : 0x80000000u;
+      }
+#pragma unroll
+      for (int hh = 0; hh < WR; ++hh) {
+        const int n = n0 + hh * 128 + r;
+        wvo[hh][i] = n < p.N ? (unsigned)(((long)n * p.K + kch[i]) * 2) : 0x80000000u;
+      }
+    }
+  }
+  auto bdma_x = [&](int kt, int buf) {
+#pragma unroll
+    for (int hh = 0; hh < XR; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (VDA_LDS void*)(smem + buf * BUF + hh * HALF + (2 * wave + i) * 8 * BK),
+                                                 16, (int)xvo[hh][i], kt * BK * 2, 0, 0);
+  };
+  auto bdma_w = [&](int kt, int buf) {
+#pragma unroll
+    for (int hh = 0; hh < WR; ++hh)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (VDA_LDS void*)(smem + buf * BUF + (XR + hh) * HALF + (2 * wave + i) * 8 * BK),
+                                                 16, (int)wvo[hh][i], kt * BK * 2, 0, 0);
+  };
 
   f4 acc[4][8];
 #pragma unroll
@@ -645,8 +684,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   const int woff = XR * HALF + (wn >> 1) * HALF;
   const int wrow0 = (wn & 1) * 64;
 
-  dma_x(0, 0);
-  dma_w(0, 0);
+  if constexpr (CONV) {
+    dma_x(0, 0);
+    dma_w(0, 0);
+  } else {
+    bdma_x(0, 0);
+    bdma_w(0, 0);
+  }
   wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   const bool lagging = wave >= 4;
@@ -696,11 +740,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     // P1
     load_x(base, 0);
     load_w(base, 0);
-    if (more) dma_x(kt + 1, nb);
+    if (more) { if constexpr (CONV) dma_x(kt + 1, nb); else bdma_x(kt + 1, nb); }
     mma(0, 0);
     // P2
     load_w(base, 1);
-    if (more) dma_w(kt + 1, nb);
+    if (more) { if constexpr (CONV) dma_w(kt + 1, nb); else bdma_w(kt + 1, nb); }
     mma(0, 1);
     // P3
     load_x(base, 1);
@@ -846,9 +890,12 @@ void launch_act(const GemmParams& p, hipStream_t st) {
                      (!e.res || ((uintptr_t)e.res % 16 == 0 && e.ldres % 8 == 0)) &&
                      (!e.res2 || ((uintptr_t)e.res2 % 16 == 0 && e.ldres2 % 8 == 0)) &&
                      (e.act != VDA_ACT_GEGLU || (p.N / 2) % 8 == 0);
-    if (p.N <= 64 || p.K <= 256) cfg = 2;
-    else if (p.N >= 256 && p.M >= 4096 && a16 && e.store == VDA_STORE_ROWS) cfg = 4;
-    else if (p.N == 128 && p.M >= 8192 && a16 && e.store == VDA_STORE_ROWS) cfg = 5;
+    // the phased kernels' dense path needs K % 64 == 0 and 32-bit buffer offsets
+    const bool dense_ok = CONV || (p.K % 64 == 0 && (long)p.M * p.ldx * 2 < (1L << 31) &&
+                                   (long)p.N * p.K * 2 < (1L << 31));
+    if (p.N <= 64 || (p.K <= 256 && p.N < 256)) cfg = 2;
+    else if (p.N >= 256 && p.M >= 4096 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 4;
+    else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 5;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
     else cfg = 0;

@@ -268,7 +268,7 @@ class VideoDepthAnything(nn.Module):
         enc = self.pretrained
         C = enc.embed_dim
         P.C, P.heads = C, enc.num_heads
-        P.Kp = 592  # 588 = 3*14*14 rounded up to a multiple of 8
+        P.Kp = 640  # 588 = 3*14*14 zero-padded to a multiple of 64 (the LDS-DMA GEMM K step)
         wpe = enc.patch_embed.proj.weight.reshape(C, -1)
         P.patch_w = _h(F.pad(wpe, (0, P.Kp - wpe.shape[1]))).to(dev)
         P.patch_b = _f(enc.patch_embed.proj.bias).to(dev)
