@@ -48,6 +48,7 @@ def parse():
                     help="frames of the bounded CPU-oracle sample (0 disables)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-launch event probe")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a captured HIP graph")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsal)")
     return ap.parse_args()
 
 
@@ -57,11 +58,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    ndev = torch.cuda.device_count()
+    local = local % max(1, ndev)  # (rehearsal with more ranks than GPUs: ranks share a device)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            tdist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        else:
+            tdist.init_process_group(args.backend)
 
     import vda_amd
     from vda_amd import ops
@@ -73,7 +79,12 @@ def main():
     if dist:
         import torch.distributed as tdist
         for t in model.state_dict().values():
-            tdist.broadcast(t, src=0)
+            if args.backend == "nccl":
+                tdist.broadcast(t, src=0)
+            else:  # gloo rehearsal: host copies
+                c = t.detach().cpu()
+                tdist.broadcast(c, src=0)
+                t.copy_(c)
         model.load_state_dict(model.state_dict(), strict=True)  # drop packs; re-pack from broadcast weights
     g = torch.Generator().manual_seed(1000 + rank)
     x = torch.randn(args.clips_per_gpu, T, 3, H, W, generator=g).to(dev)
@@ -109,12 +120,14 @@ def main():
     elapsed = time.perf_counter() - t0
     launches = ops.take_probe() if probe else {}
     if dist:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        cdev = dev if args.backend == "nccl" else torch.device("cpu")
+        tt = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
         elapsed = float(tt.item())
         # one-off (untimed) gather of the last clip's depth to rank 0: the clip-parallel output path
-        lst = [torch.empty_like(depth) for _ in range(world)] if rank == 0 else None
-        tdist.gather(depth.contiguous(), lst, dst=0)
+        dd = depth.contiguous().to(cdev)
+        lst = [torch.empty_like(dd) for _ in range(world)] if rank == 0 else None
+        tdist.gather(dd, lst, dst=0)
     frames = world * args.steps * args.clips_per_gpu * T
     value = frames / elapsed
     if not bool(torch.isfinite(depth).all()):
