@@ -57,7 +57,8 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) o[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.f, 0.f};
+  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
+  bool first = true;
 
   // staging: each thread moves 2 K chunks and 2 V chunks (16 B) per tile
   const int srow = tid >> 3, schunk = tid & 7;
@@ -89,11 +90,13 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
     constexpr bool MASK = decltype(mask_tag)::value;
     const int buf = kt & 1;
     // ---- Sᵀ = K Qᵀ : s[a][qs] lane holds keys a*16 + 4g + r, query qs*16 + li
+    // the accumulators start at -m (running max, log2 units), so s = q.k*scale - m comes out of the
+    // MFMA chain ready for exp2 (no per-score subtraction)
     f4 s[4][2];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int qs = 0; qs < 2; ++qs) s[a][qs] = f4{0.f, 0.f, 0.f, 0.f};
+      for (int qs = 0; qs < 2; ++qs) s[a][qs] = f4{-mrun[qs], -mrun[qs], -mrun[qs], -mrun[qs]};
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
@@ -121,25 +124,32 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
                            fmaxf(fmaxf(s[3][qs][0], s[3][qs][1]), fmaxf(s[3][qs][2], s[3][qs][3]))));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (__any(mx > mrun[qs])) {
-        const float mnew = fmaxf(mrun[qs], mx);
-        const float alpha = __builtin_amdgcn_exp2f(mrun[qs] - mnew);
-        mrun[qs] = mnew;
+      // mx is the tile max relative to the running max.  Deferred rescale (T13): keep the stale
+      // max while mx <= 8, i.e. P <= 2^8, exact in fp16 P / fp32 sums.  The first tile always
+      // re-bases (m starts at 0, not at a real max).
+      if (first || __any(mx > 8.f)) {
+        const float sh = first ? mx : fmaxf(mx, 0.f);
+        const float alpha = __builtin_amdgcn_exp2f(-sh);
+        mrun[qs] += sh;
         lrun[qs] *= alpha;
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[d][qs] *= alpha;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) s[a][qs] -= sh;
       }
-      const float m = mrun[qs];
-      float ps = 0.f;
+      float ps0 = 0.f, ps1 = 0.f;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[a][qs][r] - m);
-          ps += pv;
-          pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)pv;
+        for (int r = 0; r < 4; r += 2) {
+          const float p0 = __builtin_amdgcn_exp2f(s[a][qs][r]);
+          const float p1 = __builtin_amdgcn_exp2f(s[a][qs][r + 1]);
+          ps0 += p0;
+          ps1 += p1;
+          pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)p0;
+          pf[qs][a >> 1][(a & 1) * 4 + r + 1] = (h16)p1;
         }
-      lrun[qs] += ps;
+      lrun[qs] += ps0 + ps1;
     }
     // ---- Oᵀ += Vᵀ Pᵀ
     const int q4 = li >> 2, p4 = li & 3;
@@ -168,6 +178,7 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
     if (kt + 1 < ntiles) gload(kt + 1);
     if (kt < nfull) tile(kt, std::false_type{});
     else tile(kt, std::true_type{});
+    first = false;
     if (kt + 1 < ntiles) sstore((kt + 1) & 1);
     __syncthreads();
   }

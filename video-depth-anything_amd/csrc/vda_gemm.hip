@@ -763,7 +763,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     // it back as whole rows, adds the residual(s) with 16-byte loads and stores 16-byte chunks, so
     // every output row is written by full contiguous 128-B lines.
     constexpr int OW = (ACT == VDA_ACT_GEGLU) ? BN / 2 : BN;  // output columns of this tile
-    constexpr int UPR = OW / 4;                              // 8-byte units per row
     __syncthreads();                                         // all waves done with the operand image
     const vda_epilogue& e = p.epi;
 #pragma unroll
