@@ -1035,8 +1035,28 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   p.M = BT * Ho * Wo; p.N = 64; p.K = 9 * C; p.ldy = 1;
   p.epi = default_epi();
   p.epi.bias = b1; p.epi.gamma = w2; p.epi.rowbias = b2;
-  const int tiles_m = (p.M + 127) / 128;
-  hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, 32, 4, true, ACT_DEPTH>), dim3(tiles_m), dim3(256), 0, st, p, tiles_m, 1);
+  const int cfg = g_force_tile >= 10 ? g_force_tile - 10 : 3;
+  switch (cfg) {
+    case 1: {
+      const int tiles_m = (p.M + 255) / 256;
+      hipLaunchKernelGGL((gemm_kernel<256, 64, 8, 1, 64, 3, true, ACT_DEPTH>), dim3(tiles_m), dim3(512), 0, st, p, tiles_m, 1);
+      break;
+    }
+    case 2: {
+      const int tiles_m = (p.M + 511) / 512;
+      hipLaunchKernelGGL((gemm_kernel<512, 64, 8, 1, 64, 2, true, ACT_DEPTH>), dim3(tiles_m), dim3(512), 0, st, p, tiles_m, 1);
+      break;
+    }
+    case 3: {
+      const int tiles_m = (p.M + 255) / 256;
+      hipLaunchKernelGGL((gemm_kernel<256, 64, 8, 1, 64, 2, true, ACT_DEPTH>), dim3(tiles_m), dim3(512), 0, st, p, tiles_m, 1);
+      break;
+    }
+    default: {
+      const int tiles_m = (p.M + 127) / 128;
+      hipLaunchKernelGGL((gemm_kernel<128, 64, 4, 1, 32, 4, true, ACT_DEPTH>), dim3(tiles_m), dim3(256), 0, st, p, tiles_m, 1);
+    }
+  }
   VDA_LAUNCH_CHECK();
   return 0;
 }
