@@ -147,7 +147,7 @@ def main():
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic,
-                "kernel": f"gemm_kernel<128,128,Dense,GELU> enc fc1 M={M} N={4 * C} K={C}",
+                "kernel": f"gemm256_kernel<2,2,dense,GELU> (encoder fc1) M={M} N={4 * C} K={C}",
                 "flop_per_launch": flop, "avg_launch_ms": round(ms, 4), "launches": len(launches["enc_fc1"])}
 
     cpu = None
