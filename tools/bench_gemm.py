@@ -9,12 +9,13 @@ from vda_amd._lib import ACT_GELU
 L = _lib.lib()
 dev = "cuda"
 torch.manual_seed(0)
-shapes = [("qkv", 43840, 3072, 1024, 0), ("proj", 43840, 1024, 1024, 0), ("fc1", 43840, 4096, 1024, ACT_GELU),
+shapes = [("sq4k", 4096, 4096, 4096, 0), ("sq8k", 8192, 8192, 8192, 0)] if os.environ.get("SQ") else []
+shapes += [("qkv", 43840, 3072, 1024, 0), ("proj", 43840, 1024, 1024, 0), ("fc1", 43840, 4096, 1024, ACT_GELU),
           ("fc2", 43840, 1024, 4096, 0), ("mm0_qkv", 43808, 3072, 1024, 0), ("mm3_ff1", 175232, 2048, 256, 0),
           ("mm3_ff2", 175232, 256, 1024, 0)]
 cfgs = [int(c) for c in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["0", "1", "2", "3"])]
 for name, M, N, K, act in shapes:
-    x = torch.randn(M, K, device=dev, dtype=torch.float16)
+    x = torch.rand(M, K, device=dev, dtype=torch.float16) * 2 - 1
     w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
     b = torch.randn(N, device=dev) * 0.1
     ref = torch.nn.functional.gelu((x.float() @ w.float().t()) + b) if act == ACT_GELU else (x.float() @ w.float().t()) + b

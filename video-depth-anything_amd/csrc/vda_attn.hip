@@ -57,7 +57,12 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) o[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
+  float mrun[2] = {0.f, 0.f};
+  // row sums ride on the PV MFMA: an extra 16-row "Vᵀ" block whose rows 0, 4, 8, 12 are ones puts
+  // sum_k P[k][q] into register 0 of every lane group (no VALU adds, rescaled along with O)
+  f4 lsum[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+  const h16 one_or_zero = (lane & 3) == 0 ? (h16)1.f : (h16)0.f;
+  const h8 ones = h8{one_or_zero, one_or_zero, one_or_zero, one_or_zero, one_or_zero, one_or_zero, one_or_zero, one_or_zero};
   bool first = true;
 
   // staging: each thread moves 2 K chunks and 2 V chunks (16 B) per tile
@@ -118,12 +123,17 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
     h8 pf[2][2];  // [qs][kc] P fragments (B operand of PV)
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
-      float mx = fmaxf(fmaxf(fmaxf(s[0][qs][0], s[0][qs][1]), fmaxf(s[0][qs][2], s[0][qs][3])),
-                       fmaxf(fmaxf(s[1][qs][0], s[1][qs][1]), fmaxf(s[1][qs][2], s[1][qs][3])));
-      mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(s[2][qs][0], s[2][qs][1]), fmaxf(s[2][qs][2], s[2][qs][3])),
-                           fmaxf(fmaxf(s[3][qs][0], s[3][qs][1]), fmaxf(s[3][qs][2], s[3][qs][3]))));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      // 16 scores -> 8 v_max3 (the file is built with -fno-honor-nans -mno-amdgpu-ieee, so no
+      // canonicalising v_max on the MFMA results), then the 4 lane groups via permlane swaps
+      float mx = fmaxf(fmaxf(s[0][qs][0], s[0][qs][1]), s[0][qs][2]);
+      mx = fmaxf(fmaxf(mx, s[0][qs][3]), s[1][qs][0]);
+      mx = fmaxf(fmaxf(mx, s[1][qs][1]), s[1][qs][2]);
+      mx = fmaxf(fmaxf(mx, s[1][qs][3]), s[2][qs][0]);
+      mx = fmaxf(fmaxf(mx, s[2][qs][1]), s[2][qs][2]);
+      mx = fmaxf(fmaxf(mx, s[2][qs][3]), s[3][qs][0]);
+      mx = fmaxf(fmaxf(mx, s[3][qs][1]), s[3][qs][2]);
+      mx = fmaxf(mx, s[3][qs][3]);
+      mx = group_max4(mx);
       // mx is the tile max relative to the running max.  Deferred rescale (T13): keep the stale
       // max while mx <= 8, i.e. P <= 2^8, exact in fp16 P / fp32 sums.  The first tile always
       // re-bases (m starts at 0, not at a real max).
@@ -131,25 +141,16 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
         const float sh = first ? mx : fmaxf(mx, 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-sh);
         mrun[qs] += sh;
-        lrun[qs] *= alpha;
+        lsum[qs][0] *= alpha;
 #pragma unroll
         for (int d = 0; d < 4; ++d) o[d][qs] *= alpha;
 #pragma unroll
         for (int a = 0; a < 4; ++a) s[a][qs] -= sh;
       }
-      float ps0 = 0.f, ps1 = 0.f;
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const float p0 = __builtin_amdgcn_exp2f(s[a][qs][r]);
-          const float p1 = __builtin_amdgcn_exp2f(s[a][qs][r + 1]);
-          ps0 += p0;
-          ps1 += p1;
-          pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)p0;
-          pf[qs][a >> 1][(a & 1) * 4 + r + 1] = (h16)p1;
-        }
-      lrun[qs] += ps0 + ps1;
+        for (int r = 0; r < 4; ++r) pf[qs][a >> 1][(a & 1) * 4 + r] = (h16)__builtin_amdgcn_exp2f(s[a][qs][r]);
     }
     // ---- Oᵀ += Vᵀ Pᵀ
     const int q4 = li >> 2, p4 = li & 3;
@@ -166,6 +167,8 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 #pragma unroll
         for (int qs = 0; qs < 2; ++qs) o[d][qs] = mfma16(vf, pf[qs][kc], o[d][qs]);
       }
+#pragma unroll
+      for (int qs = 0; qs < 2; ++qs) lsum[qs] = mfma16(ones, pf[qs][kc], lsum[qs]);
     }
   };
 
@@ -185,10 +188,7 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
   // ---- epilogue: normalise and store (lane: d = dsub*16 + 4g + r, q = qs*16 + li)
 #pragma unroll
   for (int qs = 0; qs < 2; ++qs) {
-    float l = lrun[qs];
-    l += __shfl_xor(l, 16, 64);
-    l += __shfl_xor(l, 32, 64);
-    const float inv = 1.f / l;
+    const float inv = 1.f / lsum[qs][0];
     const int q = blockIdx.x * SQB + wave * 32 + qs * 16 + li;
     if (q < N) {
       h16* op = out + ((long)b * N + q) * C + h * SD;

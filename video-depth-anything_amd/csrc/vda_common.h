@@ -19,7 +19,12 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 #define VDA_LDS __attribute__((address_space(3)))
 
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
+#ifdef VDA_MFMA_BF16  // power/clock experiments only (tools/bf16_probe.py)
+  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ f16x mfma32(h8 a, h8 b, f16x c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -61,6 +66,14 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
+}
+
+// max over the 4 lane groups of 16 (lane bits 4 and 5) with VALU permlane swaps, no LDS traffic
+__device__ __forceinline__ float group_max4(float v) {
+  const auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+  v = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
+  return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
 }
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }

@@ -544,19 +544,23 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
-  // this lane's DMA rows: pieces 2*wave and 2*wave+1 of every half-tile region
+  // DMA quarters: every operand region is staged as two quarters, each refilled in its own phase
+  // (the rows one quadrant of the wave tiles reads).  X quarter i = rows 64i..64i+63 of every X
+  // region, W quarter i = rows {32i..32i+31, 64+32i..64+32i+31} of every W region; in each, wave
+  // w moves one 8-row piece (1 KiB) per region: this lane's row is xr_of(i) / wr_of(i).
   const h16* xrow[XR][2];
   const h16* wrow[WR][2];
   bool xok[XR][2], wok[WR][2];
-  int kch[2];
+  auto xr_of = [&](int i) { return i * 64 + wave * 8 + (lane >> 3); };
+  auto wr_of = [&](int i) { return (wave >> 2) * 64 + i * 32 + (wave & 3) * 8 + (lane >> 3); };
+  // row bits 0-3 are (wave & 1, lane >> 3) for both layouts, so the source swizzle is one value
+  const int kch0 = ((lane & 7) ^ ((((wave & 1) << 3 | (lane >> 3)) >> 1) & 7)) * 8;
   int cyx[XR][2];  // conv: top-left input (row << 16 | col & 0xffff) of the output pixel's window
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int r = (2 * wave + i) * 8 + (lane >> 3);
-    kch[i] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
 #pragma unroll
     for (int hh = 0; hh < XR; ++hh) {
-      const int m = m0 + hh * 128 + r;
+      const int m = m0 + hh * 128 + xr_of(i);
       xok[hh][i] = m < p.M;
       const int mm = xok[hh][i] ? m : 0;
       if constexpr (CONV) {
@@ -573,7 +577,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     }
 #pragma unroll
     for (int hh = 0; hh < WR; ++hh) {
-      const int n = n0 + hh * 128 + r;
+      const int n = n0 + hh * 128 + wr_of(i);
       wok[hh][i] = n < p.N;
       wrow[hh][i] = p.w + (long)(wok[hh][i] ? n : 0) * p.K;
     }
@@ -582,7 +586,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   // conv: when Cin % 64 == 0 a K tile never straddles a tap, so the tap is wave-uniform (scalar
   // math) and a lane only adds a scalar offset to its window base; otherwise per-lane division.
   const bool tap_uniform = CONV && (p.Cin % BK == 0);
-  auto dma_x = [&](int kt, int buf) {
+  auto dma_x = [&](int kt, int buf, int i) {
     const int k0 = kt * BK;
     int ky = 0, kx = 0, ci0 = 0;
     long toff = 0;
@@ -594,17 +598,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
       toff = ((long)ky * p.W + kx) * p.Cin + ci0;
     }
 #pragma unroll
-    for (int hh = 0; hh < XR; ++hh)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = k0 + kch[i];
+    for (int hh = 0; hh < XR; ++hh) {
+        const int k = k0 + kch0;
         const void* src = zero;
         if constexpr (CONV) {
           if (k < p.K) {
             if (tap_uniform) {
               if ((unsigned)((cyx[hh][i] >> 16) + ky) < (unsigned)p.H &&
                   (unsigned)((short)(cyx[hh][i] & 0xffff) + kx) < (unsigned)p.W)
-                src = xrow[hh][i] + toff + kch[i];
+                src = xrow[hh][i] + toff + kch0;
             } else {
               const int tap = k / p.Cin, ci = k - tap * p.Cin;
               const int ty = tap / p.ks, tx = tap - ty * p.ks;
@@ -616,19 +618,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
         } else if (xok[hh][i] && k < p.K) {
           src = xrow[hh][i] + k;
         }
-        glds16(src, smem + buf * BUF + hh * HALF + (2 * wave + i) * 8 * BK);
-      }
+        glds16(src, smem + buf * BUF + hh * HALF + (xr_of(i) - (lane >> 3)) * BK);
+    }
   };
-  auto dma_w = [&](int kt, int buf) {
+  auto dma_w = [&](int kt, int buf, int i) {
     const int k0 = kt * BK;
 #pragma unroll
-    for (int hh = 0; hh < WR; ++hh)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int k = k0 + kch[i];
-        const void* src = (wok[hh][i] && k < p.K) ? (const void*)(wrow[hh][i] + k) : zero;
-        glds16(src, smem + buf * BUF + (XR + hh) * HALF + (2 * wave + i) * 8 * BK);
-      }
+    for (int hh = 0; hh < WR; ++hh) {
+      const int k = k0 + kch0;
+      const void* src = (wok[hh][i] && k < p.K) ? (const void*)(wrow[hh][i] + k) : zero;
+      glds16(src, smem + buf * BUF + (XR + hh) * HALF + (wr_of(i) - (lane >> 3)) * BK);
+    }
   };
   // Dense GEMMs (K % 64 == 0, operands < 4 GiB): buffer_load ... lds with a per-lane byte offset
   // that never changes (row, chunk) and the K advance in the scalar soffset, so issuing a piece
@@ -640,35 +640,32 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     wrs = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)(unsigned)((long)p.N * p.K * 2), 0x00020000);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int r = (2 * wave + i) * 8 + (lane >> 3);
 #pragma unroll
       for (int hh = 0; hh < XR; ++hh) {
-        const int m = m0 + hh * 128 + r;
-        xvo[hh][i] = m < p.M ? (unsigned)(((long)m * p.ldx + kch[i]) * 2) : 0x80000000u;
+        const int m = m0 + hh * 128 + xr_of(i);
+        xvo[hh][i] = m < p.M ? (unsigned)(((long)m * p.ldx + kch0) * 2) : 0x80000000u;
       }
 #pragma unroll
       for (int hh = 0; hh < WR; ++hh) {
-        const int n = n0 + hh * 128 + r;
-        wvo[hh][i] = n < p.N ? (unsigned)(((long)n * p.K + kch[i]) * 2) : 0x80000000u;
+        const int n = n0 + hh * 128 + wr_of(i);
+        wvo[hh][i] = n < p.N ? (unsigned)(((long)n * p.K + kch0) * 2) : 0x80000000u;
       }
     }
   }
-  auto bdma_x = [&](int kt, int buf) {
+  auto bdma_x = [&](int kt, int buf, int i) {
 #pragma unroll
     for (int hh = 0; hh < XR; ++hh)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (VDA_LDS void*)(smem + buf * BUF + hh * HALF + (2 * wave + i) * 8 * BK),
-                                                 16, (int)xvo[hh][i], kt * BK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (VDA_LDS void*)(smem + buf * BUF + hh * HALF + (xr_of(i) - (lane >> 3)) * BK),
+                                               16, (int)xvo[hh][i], kt * BK * 2, 0, 0);
   };
-  auto bdma_w = [&](int kt, int buf) {
+  auto bdma_w = [&](int kt, int buf, int i) {
 #pragma unroll
     for (int hh = 0; hh < WR; ++hh)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (VDA_LDS void*)(smem + buf * BUF + (XR + hh) * HALF + (2 * wave + i) * 8 * BK),
-                                                 16, (int)wvo[hh][i], kt * BK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (VDA_LDS void*)(smem + buf * BUF + (XR + hh) * HALF + (wr_of(i) - (lane >> 3)) * BK),
+                                               16, (int)wvo[hh][i], kt * BK * 2, 0, 0);
   };
+  auto stage_x = [&](int kt, int buf, int i) { if constexpr (CONV) dma_x(kt, buf, i); else bdma_x(kt, buf, i); };
+  auto stage_w = [&](int kt, int buf, int i) { if constexpr (CONV) dma_w(kt, buf, i); else bdma_w(kt, buf, i); };
 
   f4 acc[4][8];
 #pragma unroll
@@ -684,14 +681,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   const int woff = XR * HALF + (wn >> 1) * HALF;
   const int wrow0 = (wn & 1) * 64;
 
-  if constexpr (CONV) {
-    dma_x(0, 0);
-    dma_w(0, 0);
+  // prologue: all of tile 0, then the two tile-1 quarters the loop expects from "tile -1"
+  stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
+  if (nk > 1) {
+    stage_x(1, 1, 0); stage_w(1, 1, 1);
+    wait_vmcnt<XR + WR>();
   } else {
-    bdma_x(0, 0);
-    bdma_w(0, 0);
+    wait_vmcnt<0>();
   }
-  wait_vmcnt<0>();
   __builtin_amdgcn_s_barrier();
   const bool lagging = wave >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();  // stagger waves 4-7 by one barrier
@@ -733,25 +730,34 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     __builtin_amdgcn_s_barrier();
   };
 
+  // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
+  // and retired by the P4 wait one phase before its first read:
+  //   P1: Xq1(t+1) -> other buffer   P2: Wq0(t+1) -> other   P3: Xq0(t+2) -> this   P4: Wq1(t+2) -> this
   for (int kt = 0; kt < nk; ++kt) {
-    const h16* base = smem + (kt & 1) * BUF;
-    const int nb = (kt + 1) & 1;
-    const bool more = kt + 1 < nk;
+    const int cb = kt & 1, nb = cb ^ 1;
+    const h16* base = smem + cb * BUF;
+    const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
     // P1
     load_x(base, 0);
     load_w(base, 0);
-    if (more) { if constexpr (CONV) dma_x(kt + 1, nb); else bdma_x(kt + 1, nb); }
+    if (more1) stage_x(kt + 1, nb, 1);
     mma(0, 0);
     // P2
     load_w(base, 1);
-    if (more) { if constexpr (CONV) dma_w(kt + 1, nb); else bdma_w(kt + 1, nb); }
+    if (more1) stage_w(kt + 1, nb, 0);
     mma(0, 1);
     // P3
     load_x(base, 1);
+    if (more2) stage_x(kt + 2, cb, 0);
     mma(1, 1);
-    // P4
+    // P4: retire everything but this tile's two P3/P4 quarters
     load_w(base, 0);
-    wait_vmcnt<0>();
+    if (more2) {
+      stage_w(kt + 2, cb, 1);
+      wait_vmcnt<XR + WR>();
+    } else {
+      wait_vmcnt<0>();
+    }
     mma(1, 0);
   }
   if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
