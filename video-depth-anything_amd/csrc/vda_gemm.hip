@@ -585,17 +585,22 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   const void* zero = (const void*)g_zero_page;
   // conv: when Cin % 64 == 0 a K tile never straddles a tap, so the tap is wave-uniform (scalar
   // math) and a lane only adds a scalar offset to its window base; otherwise per-lane division.
+  // Each X quarter is staged for K tiles 0, 1, 2, ... in order, so its tap (ky, kx) and window
+  // offset advance incrementally (no per-tile division): +BK channels, +(W - ks) * Cin on a row wrap.
   const bool tap_uniform = CONV && (p.Cin % BK == 0);
+  int t_ci[2] = {0, 0}, t_kx[2] = {0, 0}, t_ky[2] = {0, 0};
+  long t_off[2] = {0, 0};
   auto dma_x = [&](int kt, int buf, int i) {
     const int k0 = kt * BK;
-    int ky = 0, kx = 0, ci0 = 0;
-    long toff = 0;
+    const int ky = t_ky[i], kx = t_kx[i];
+    const long toff = t_off[i];
     if (tap_uniform) {
-      const int tap = k0 / p.Cin;
-      ci0 = k0 - tap * p.Cin;
-      ky = tap / p.ks;
-      kx = tap - ky * p.ks;
-      toff = ((long)ky * p.W + kx) * p.Cin + ci0;
+      t_off[i] += BK;
+      t_ci[i] += BK;
+      if (t_ci[i] == p.Cin) {
+        t_ci[i] = 0;
+        if (++t_kx[i] == p.ks) { t_kx[i] = 0; ++t_ky[i]; t_off[i] += (long)(p.W - p.ks) * p.Cin; }
+      }
     }
 #pragma unroll
     for (int hh = 0; hh < XR; ++hh) {
