@@ -14,7 +14,7 @@ all: $(PKG)/libvda.so
 # off the MFMA results instead of canonicalising v_max per score)
 build/vda_attn.o: EXTRA := -fno-honor-nans -mno-amdgpu-ieee
 
-build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h include/vda.h
+build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h $(PKG)/csrc/phi_table.h include/vda.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) $(EXTRA) -c $< -o $@
 

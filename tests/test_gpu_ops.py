@@ -78,9 +78,10 @@ def test_gemm_strided_rows():
     assert rel(y, big[:, K:2 * K] @ w.t()) < 2e-3
 
 
-@pytest.mark.parametrize("k,cin,cout", [(4, 48, 48), (2, 96, 96), (4, 256, 256)])
-def test_conv_transpose_pixel_shuffle(k, cin, cout):
-    BT, hh, ww = 3, 5, 7
+@pytest.mark.parametrize("k,cin,cout,BT,hh,ww", [(4, 48, 48, 3, 5, 7), (2, 96, 96, 3, 5, 7), (4, 256, 256, 3, 5, 7),
+                                                  # large M: the phased 256x256 kernel with the pixel-shuffle store
+                                                  (4, 256, 256, 4, 37, 37), (2, 512, 512, 4, 37, 37)])
+def test_conv_transpose_pixel_shuffle(k, cin, cout, BT, hh, ww):
     x = rnd(BT, cin, hh, ww, seed=15)
     w = rnd(cin, cout, k, k, scale=cin ** -0.5, seed=16)
     b = rnd(cout, scale=0.1, seed=17)

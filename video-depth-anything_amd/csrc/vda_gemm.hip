@@ -16,6 +16,7 @@
 // are 128 B (64 halfs) with the 16-B chunk index XOR-swizzled by (row>>1)&7, which makes both the
 // ds_write_b128 stores and the 16-lane ds_read_b128 fragment reads bank-conflict free.
 #include "vda_common.h"
+#include "phi_table.h"
 #include "../../include/vda.h"
 
 namespace {
@@ -319,6 +320,17 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
   tn = in_group / gsize;
 }
 
+// gelu(x) = x * Phi(x), Phi linearly interpolated from the LDS copy of phi_table.h (1/128 steps on
+// [-8, 8], clamped outside): |error| <= 2.2e-6 absolute, far below the fp16 output rounding, for
+// about half the issue cycles of the erf form (which needs a v_rcp and a v_exp per element).
+__device__ __forceinline__ float gelu_tab(float x, const float* tab) {
+  const float u = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, 1024.f), 0.f, 2048.f);
+  const int i = min((int)u, 2047);
+  const float t = u - (float)i;
+  const float2 ab = *reinterpret_cast<const float2*>(tab + 2 * i);
+  return x * fmaf(t, ab.y, ab.x);
+}
+
 __device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
 }
@@ -535,7 +547,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   constexpr int BM = 128 * XR, BN = 128 * WR;
   constexpr int HALF = 128 * BK;            // halfs per 128-row region (16 KiB)
   constexpr int BUF = (XR + WR) * HALF;     // one K tile
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF];
+  // GELU / GEGLU epilogues read Phi from a 16-KiB LDS table (phi_table.h) staged in the prologue
+  constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0)];
+  const float* phi_lds = reinterpret_cast<const float*>(smem + 2 * BUF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -686,7 +701,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   const int woff = XR * HALF + (wn >> 1) * HALF;
   const int wrow0 = (wn & 1) * 64;
 
-  // prologue: all of tile 0, then the two tile-1 quarters the loop expects from "tile -1"
+  // prologue: [Phi table,] all of tile 0, then the two tile-1 quarters the loop expects from "tile -1"
+  if constexpr (TAB) {
+    const char* src = reinterpret_cast<const char*>(g_phi_tab) + tid * 16;
+    glds16(src, smem + 2 * BUF + wave * 512);
+    glds16(src + 8192, smem + 2 * BUF + 4096 + wave * 512);
+  }
   stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
   if (nk > 1) {
     stage_x(1, 1, 0); stage_w(1, 1, 1);
@@ -776,40 +796,68 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     constexpr int OW = (ACT == VDA_ACT_GEGLU) ? BN / 2 : BN;  // output columns of this tile
     __syncthreads();                                         // all waves done with the operand image
     const vda_epilogue& e = p.epi;
+    // Per-channel operands are loaded ONCE per lane, unconditionally from clamped addresses, before
+    // any math: a load under a per-element condition makes hipcc branch around it and wait for
+    // each one in turn (32 dependent L2 round trips per tile).
+    bool nok[4];
+    int ncl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + nq;
+      nok[i] = n < p.N;
+      ncl[i] = nok[i] ? n : 0;
+    }
+    if (e.bias) {  // bias folded into the accumulators up front (GEGLU: h and g halves alike)
+      f4 bv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        bv[i] = *reinterpret_cast<const f4*>(e.bias + (ACT == VDA_ACT_GEGLU ? ncl[i & ~1] + (i & 1) * 16 : ncl[i]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] += bv[i];
+    }
+    if constexpr (ACT != VDA_ACT_GEGLU) {
+      if (e.rowbias) {  // per-row bias (folded positional terms): 4 loads per output row group
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int m = m0 + wm * 128 + j * 16 + mcol;
+          const long roff = m < p.M ? (long)((m / e.rdiv) % e.rmod) * p.N : 0;
+          f4 rb[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rb[i] = *reinterpret_cast<const f4*>(e.rowbias + roff + ncl[i]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] += rb[i];
+        }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; i += (ACT == VDA_ACT_GEGLU ? 2 : 1)) {
       const int nl = wn * 64 + i * 16 + nq;  // local W row of this lane's first channel
-      const int n = n0 + nl;
+      f4 gv = f4{1.f, 1.f, 1.f, 1.f};
+      if (e.gamma)
+        gv = *reinterpret_cast<const f4*>(e.gamma + (ACT == VDA_ACT_GEGLU ? (nok[i] ? (n0 >> 1) + ((wn * 64 + i * 16) >> 1) + nq : 0) : ncl[i]));
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int ml = wm * 128 + j * 16 + mcol;
-        const int m = m0 + ml;
         f4 v;
         int col;
         if constexpr (ACT == VDA_ACT_GEGLU) {
-          f4 vh = acc[i][j], vg = acc[i + 1][j];
-          if (e.bias && n < p.N) {
-            vh += *reinterpret_cast<const f4*>(e.bias + n);
-            vg += *reinterpret_cast<const f4*>(e.bias + n + 16);
-          }
+          const f4 vh = acc[i][j], vg = acc[i + 1][j];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = vh[r] * gelu_erf(vg[r]);
+          for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phi_lds) : gelu_erf(vg[r]));
+          v *= gv;
           col = ((wn * 64 + i * 16) >> 1) + nq;
-          if (e.gamma && n < p.N) v *= *reinterpret_cast<const f4*>(e.gamma + (n0 >> 1) + col);
         } else {
           v = acc[i][j];
-          if (n < p.N) {
-            if (e.bias) v += *reinterpret_cast<const f4*>(e.bias + n);
-            if (e.rowbias && m < p.M) v += *reinterpret_cast<const f4*>(e.rowbias + (long)((m / e.rdiv) % e.rmod) * p.N + n);
-          }
           if constexpr (ACT == VDA_ACT_GELU) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+            for (int r = 0; r < 4; ++r) v[r] = TAB ? gelu_tab(v[r], phi_lds) : gelu_erf(v[r]);
           } else if constexpr (ACT == VDA_ACT_RELU) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
           }
-          if (e.gamma && n < p.N) v *= *reinterpret_cast<const f4*>(e.gamma + n);
+          v *= gv;
           col = nl;
         }
         h4 o;
@@ -823,12 +871,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     const int nout = (ACT == VDA_ACT_GEGLU) ? (p.N >> 1) : p.N;
     const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
     constexpr int CPR = OW / 8;  // 16-byte chunks per row
-#pragma unroll 4
+    // no branch around the residual loads (clamped rows instead), only the store is predicated
+#pragma unroll 8
     for (int idx = tid; idx < BM * CPR; idx += 512) {
       const int row = idx / CPR, q = idx - row * CPR;
-      const int m = m0 + row;
-      const int c = cout0 + q * 8;
-      if (m >= p.M || c >= nout) continue;
+      const int c0 = cout0 + q * 8;
+      const bool ok = (m0 + row) < p.M && c0 < nout;
+      const int m = ok ? m0 + row : m0, c = ok ? c0 : cout0;
       const int s = row & 15;
       const uint4 raw = *reinterpret_cast<const uint4*>(&smem[row * OW + ((2 * q) ^ (s & ~1)) * 4]);
       h8 t = __builtin_bit_cast(h8, (s & 1) ? make_uint4(raw.z, raw.w, raw.x, raw.y) : raw);
@@ -849,7 +898,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
 #pragma unroll
         for (int r = 0; r < 8; ++r) t[r] = (h16)f[r];
       }
-      stg16(p.y + (long)m * p.ldy + c, __builtin_bit_cast(uint4, t));
+      if (ok) stg16(p.y + (long)m * p.ldy + c, __builtin_bit_cast(uint4, t));
     }
     return;
   }
@@ -904,7 +953,7 @@ void launch_act(const GemmParams& p, hipStream_t st) {
     const bool dense_ok = CONV || (p.K % 64 == 0 && (long)p.M * p.ldx * 2 < (1L << 31) &&
                                    (long)p.N * p.K * 2 < (1L << 31));
     if (p.N <= 64 || (p.K <= 256 && p.N < 256)) cfg = 2;
-    else if (p.N >= 256 && p.M >= 4096 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 4;
+    else if (p.N >= 256 && p.M >= 4096 && dense_ok && (e.store != VDA_STORE_ROWS || a16)) cfg = 4;
     else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 5;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
