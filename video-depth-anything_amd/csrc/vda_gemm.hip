@@ -17,6 +17,7 @@
 // ds_write_b128 stores and the 16-lane ds_read_b128 fragment reads bank-conflict free.
 #include "vda_common.h"
 #include "phi_table.h"
+#include <type_traits>
 #include "../../include/vda.h"
 
 namespace {
@@ -324,9 +325,9 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
 // [-8, 8], clamped outside): |error| <= 2.2e-6 absolute, far below the fp16 output rounding, for
 // about half the issue cycles of the erf form (which needs a v_rcp and a v_exp per element).
 __device__ __forceinline__ float gelu_tab(float x, const float* tab) {
-  const float u = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, 1024.f), 0.f, 2048.f);
-  const int i = min((int)u, 2047);
-  const float t = u - (float)i;
+  const float u = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, 1024.f), 0.f, 2047.9998f);  // < 2048: i <= 2047
+  const int i = (int)u;
+  const float t = __builtin_amdgcn_fractf(u);
   const float2 ab = *reinterpret_cast<const float2*>(tab + 2 * i);
   return x * fmaf(t, ab.y, ab.x);
 }
@@ -870,36 +871,49 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     __syncthreads();
     const int nout = (ACT == VDA_ACT_GEGLU) ? (p.N >> 1) : p.N;
     const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
-    constexpr int CPR = OW / 8;  // 16-byte chunks per row
-    // no branch around the residual loads (clamped rows instead), only the store is predicated
-#pragma unroll 8
-    for (int idx = tid; idx < BM * CPR; idx += 512) {
-      const int row = idx / CPR, q = idx - row * CPR;
-      const int c0 = cout0 + q * 8;
-      const bool ok = (m0 + row) < p.M && c0 < nout;
-      const int m = ok ? m0 + row : m0, c = ok ? c0 : cout0;
-      const int s = row & 15;
-      const uint4 raw = *reinterpret_cast<const uint4*>(&smem[row * OW + ((2 * q) ^ (s & ~1)) * 4]);
-      h8 t = __builtin_bit_cast(h8, (s & 1) ? make_uint4(raw.z, raw.w, raw.x, raw.y) : raw);
-      if (e.res || e.res2) {
-        float f[8];
+    // Phase 2: thread -> fixed (row0 + RPI * it, 16-byte chunk q).  Every iteration reuses the same
+    // LDS swizzle and advances both addresses by constants; stores (and residual loads) are buffer
+    // ops whose range check drops rows >= M and chunks >= nout (offset 0x80000000), so the loop
+    // has no branches and no per-iteration address math beyond one add.  Residuals are added in
+    // packed fp16 (one rounding per add, as the reference's fp16 adds).
+    constexpr int CPR = OW / 8;    // 16-byte chunks per row
+    constexpr int RPI = 512 / CPR; // rows per iteration (a multiple of 16: the swizzle repeats)
+    constexpr int NIT = BM / RPI;
+    const int q = tid % CPR, row0 = tid / CPR;
+    const int sw = row0 & 15;
+    const h16* l0 = smem + row0 * OW + ((2 * q) ^ sw) * 4;
+    const h16* l1 = smem + row0 * OW + ((2 * q + 1) ^ sw) * 4;
+    const int c = cout0 + q * 8;
+    const long mrows = p.M - m0;
+    auto rsrc = [&](const h16* base, long ld) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)m0 * ld), (short)0,
+                                               (int)(mrows * ld * 2 < 0x7fffffffL ? mrows * ld * 2 : 0x7fffffffL), 0x00020000);
+    };
+    auto voff = [&](long ld) { return c < nout ? (unsigned)(((long)row0 * ld + c) * 2) : 0x80000000u; };
+    const __amdgpu_buffer_rsrc_t ry = rsrc(p.y, p.ldy);
+    const unsigned vy = voff(p.ldy), sy = (unsigned)(RPI * p.ldy * 2);
+    const h16* r1p = (const h16*)(e.res ? e.res : e.res2);
+    const long r1ld = e.res ? e.ldres : e.ldres2;
+    const int nres = (e.res ? 1 : 0) + (e.res2 ? 1 : 0);
+    auto phase2 = [&](auto nres_tag) {
+      constexpr int NR = decltype(nres_tag)::value;
+      __amdgpu_buffer_rsrc_t rr1, rr2;
+      unsigned vr1 = 0, sr1 = 0, vr2 = 0, sr2 = 0;
+      if constexpr (NR >= 1) { rr1 = rsrc(r1p, r1ld); vr1 = voff(r1ld); sr1 = (unsigned)(RPI * r1ld * 2); }
+      if constexpr (NR >= 2) { rr2 = rsrc((const h16*)e.res2, e.ldres2); vr2 = voff(e.ldres2); sr2 = (unsigned)(RPI * e.ldres2 * 2); }
 #pragma unroll
-        for (int r = 0; r < 8; ++r) f[r] = (float)t[r];
-        if (e.res) {
-          const h8 a = __builtin_bit_cast(h8, ldg16((const h16*)e.res + (long)m * e.ldres + c));
-#pragma unroll
-          for (int r = 0; r < 8; ++r) f[r] += (float)a[r];
-        }
-        if (e.res2) {
-          const h8 a = __builtin_bit_cast(h8, ldg16((const h16*)e.res2 + (long)m * e.ldres2 + c));
-#pragma unroll
-          for (int r = 0; r < 8; ++r) f[r] += (float)a[r];
-        }
-#pragma unroll
-        for (int r = 0; r < 8; ++r) t[r] = (h16)f[r];
+      for (int it = 0; it < NIT; ++it) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
+        const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
+        h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        if constexpr (NR >= 1) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, vr1 + it * sr1, 0, 0));
+        if constexpr (NR >= 2) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, vr2 + it * sr2, 0, 0));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, 0);
       }
-      if (ok) stg16(p.y + (long)m * p.ldy + c, __builtin_bit_cast(uint4, t));
-    }
+    };
+    if (nres == 0) phase2(std::integral_constant<int, 0>{});
+    else if (nres == 1) phase2(std::integral_constant<int, 1>{});
+    else phase2(std::integral_constant<int, 2>{});
     return;
   }
   if constexpr (ACT == VDA_ACT_GEGLU) {
