@@ -13,6 +13,8 @@ all: $(PKG)/libvda.so
 # attention: no NaN inputs by construction, so max chains need no IEEE quieting (v_max3 straight
 # off the MFMA results instead of canonicalising v_max per score)
 build/vda_attn.o: EXTRA := -fno-honor-nans -mno-amdgpu-ieee
+# GEMM epilogues: SLP packing of scalar f32 math needs register moves that cost more than it saves
+build/vda_gemm.o: EXTRA := -fno-slp-vectorize
 
 build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h $(PKG)/csrc/phi_table.h include/vda.h
 	@mkdir -p build

@@ -165,6 +165,13 @@ int vda_depth_head(const void* x, const void* w1, const float* b1, const float* 
  */
 int vda_debug_force_tile(int32_t cfg);
 
+/*
+ * Tuning hook for the phased 256-row GEMM: persist_blocks > 0 launches that many persistent blocks
+ * (0 = one block per tile, -1 = automatic: one per CU); stagger_ticks >= 0 forces the start delay
+ * (100 MHz ticks) of the delayed half of the blocks (-1 = automatic).  Process-global; for tuning.
+ */
+int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@ sed -i 's|../../include/vda.h|vda.h|' $D/csrc/*.hip
 OBJS=""
 for f in $D/csrc/*.hip; do
   X=""; [ "$(basename $f)" = vda_attn.hip ] && X="-fno-honor-nans -mno-amdgpu-ieee"
+  [ "$(basename $f)" = vda_gemm.hip ] && X="-fno-slp-vectorize"
   /opt/rocm/bin/hipcc $FL $X -I $D/include -c $f -o ${f%.hip}.o & OBJS="$OBJS ${f%.hip}.o"
 done
 wait

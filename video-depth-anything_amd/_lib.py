@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so"
 EXPORTED = (
     "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
-    "vda_depth_head", "vda_debug_force_tile",
+    "vda_depth_head", "vda_debug_force_tile", "vda_debug_gemm_sched",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -62,8 +62,11 @@ def _declare(lib):
         "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
         "vda_depth_head": ([P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_debug_force_tile": ([I], I),
+        "vda_debug_gemm_sched": ([I, I], I),
     }
     for name, (args, res) in sig.items():
+        if name.startswith("vda_debug_") and not hasattr(lib, name):
+            continue  # tuning hooks may be absent from an older library under A/B comparison
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -82,6 +85,10 @@ def lib():
     try:
         l = ctypes.CDLL(LIB_PATH)
         _declare(l)
+        sched = os.environ.get("VDA_GEMM_SCHED")  # tuning: "persist_blocks,stagger_ticks"
+        if sched and hasattr(l, "vda_debug_gemm_sched"):
+            pb, st = (int(v) for v in sched.split(","))
+            l.vda_debug_gemm_sched(pb, st)
     except OSError as e:  # pragma: no cover - depends on the runtime
         _load_error = f"failed to load {LIB_PATH}: {e}"
         raise VDAUnavailable(_load_error) from e

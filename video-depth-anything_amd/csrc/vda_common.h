@@ -80,12 +80,13 @@ __device__ __forceinline__ float group_max4(float v) {
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ void stg16(void* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 
-__device__ __forceinline__ uint4 relu_h8(uint4 v) {
-  h8 x = __builtin_bit_cast(h8, v);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = x[j] > (h16)0 ? x[j] : (h16)0;
-  return __builtin_bit_cast(uint4, x);
+// ReLU on fp16 bit patterns: a negative half is a negative int16, so max_i16(x, 0) is relu(x)
+// (-0 and negative NaNs -> +0).  Packed: one v_pk_max_i16 per two values, no SLP pass needed.
+typedef short s8v __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ h8 relu8(h8 x) {
+  return __builtin_bit_cast(h8, __builtin_elementwise_max(__builtin_bit_cast(s8v, x), s8v{0, 0, 0, 0, 0, 0, 0, 0}));
 }
+__device__ __forceinline__ uint4 relu_h8(uint4 v) { return __builtin_bit_cast(uint4, relu8(__builtin_bit_cast(h8, v))); }
 
 // Error reporting across the C ABI (never throws).
 int vda_set_error(int code, const char* msg);

@@ -18,6 +18,15 @@
 #include "vda_common.h"
 #include "phi_table.h"
 #include <type_traits>
+#ifdef VDA_TS  // phase timestamps of each block's first phased tile (tools/ts_probe.py; experiments only)
+__device__ unsigned long long g_ts[1024][8];
+#define TS(k) do { if (threadIdx.x == 0 && vb < (int)gridDim.x && blockIdx.x < 1024) g_ts[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+extern "C" int vda_debug_timestamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ts), sizeof(g_ts), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define TS(k) do {} while (0)
+#endif
 #include "../../include/vda.h"
 
 namespace {
@@ -466,10 +475,7 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         bf[j] = *reinterpret_cast<const h8*>(&sX[swzk<KB>(wm * WTM + j * 16 + frow, ks * 4 + fchunk)]);
-        if (prerelu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) bf[j][e] = bf[j][e] > (h16)0 ? bf[j][e] : (h16)0;
-        }
+        if (prerelu) bf[j] = relu8(bf[j]);
       }
 #pragma unroll
       for (int i = 0; i < TN; ++i)
@@ -542,22 +548,27 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 // their LDS-read segment and their MFMA segment.  Restaging a region is >= 2 phases after its
 // last read and the DMA wait is one phase before the first read of the new tile (the margins the
 // stagger needs).  Raw s_barrier + explicit waits only: nothing drains the DMA queue implicitly.
-template <int XR, int WR, bool CONV, int ACT>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
-__global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n) {
+template <int XR, int WR, bool CONV, int ACT, bool ROWB>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
+__device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem) {
+  // ROWB: per-row bias support (a separate instantiation: its row-index division would otherwise
+  // raise the register pressure of every phased GEMM past the spill point)
   static_assert(XR * WR == 4 && (XR == 2 || XR == 4), "8 waves as XR (m) x 8/XR (n), wave tile 128 x 64");
   constexpr int BM = 128 * XR, BN = 128 * WR;
   constexpr int HALF = 128 * BK;            // halfs per 128-row region (16 KiB)
   constexpr int BUF = (XR + WR) * HALF;     // one K tile
   // GELU / GEGLU epilogues read Phi from a 16-KiB LDS table (phi_table.h) staged in the prologue
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0)];
   const float* phi_lds = reinterpret_cast<const float*>(smem + 2 * BUF);
 
-  const int tid = threadIdx.x, lane = tid & 63;
+  // thread id laundered through a volatile move: every lane-derived address below is recomputed
+  // per tile instead of being hoisted out of the persistent tile loop (and spilled across it)
+  int tid;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+  const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave % XR, wn = wave / XR;
   int tile_m, tile_n;
-  tile_coords(blockIdx.x, gridDim.x, tiles_m, tiles_n, tile_m, tile_n);
+  tile_coords(vb, tiles_m * tiles_n, tiles_m, tiles_n, tile_m, tile_n);
   const int m0 = tile_m * BM, n0 = tile_n * BN;
 
   // DMA quarters: every operand region is staged as two quarters, each refilled in its own phase
@@ -708,6 +719,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     glds16(src, smem + 2 * BUF + wave * 512);
     glds16(src + 8192, smem + 2 * BUF + 4096 + wave * 512);
   }
+  TS(1);
   stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
   if (nk > 1) {
     stage_x(1, 1, 0); stage_w(1, 1, 1);
@@ -716,6 +728,30 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     wait_vmcnt<0>();
   }
   __builtin_amdgcn_s_barrier();
+  TS(2);
+  // Dense GEMMs: the epilogue's per-channel bias / gamma are fetched now, under the main loop,
+  // instead of costing a dependent L2/MALL round trip after it (convs: no VGPR room, loaded later).
+  constexpr bool PREF = !CONV && !ROWB;
+  f4 pbv[4], pgv[4];
+  if constexpr (PREF) {
+    const vda_epilogue& e = p.epi;
+    const int nq0 = (lane >> 4) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + nq0;
+      const int nc = n < p.N ? n : 0;
+      pbv[i] = f4{0.f, 0.f, 0.f, 0.f};
+      pgv[i] = f4{1.f, 1.f, 1.f, 1.f};
+      if (e.bias) pbv[i] = *reinterpret_cast<const f4*>(e.bias + (ACT == VDA_ACT_GEGLU ? (n0 + wn * 64 + (i & ~1) * 16 + nq0 < p.N ? n0 + wn * 64 + (i & ~1) * 16 + nq0 : 0) + (i & 1) * 16 : nc));
+      if (e.gamma) {
+        if constexpr (ACT == VDA_ACT_GEGLU) {
+          if (i % 2 == 0) pgv[i] = *reinterpret_cast<const f4*>(e.gamma + (n < p.N ? (n0 >> 1) + ((wn * 64 + i * 16) >> 1) + nq0 : 0));
+        } else {
+          pgv[i] = *reinterpret_cast<const f4*>(e.gamma + nc);
+        }
+      }
+    }
+  }
   const bool lagging = wave >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();  // stagger waves 4-7 by one barrier
 
@@ -726,10 +762,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         xf[j][ks] = *reinterpret_cast<const h8*>(&base[xoff + swz(qm * 64 + j * 16 + frow, ks * 4 + fchunk)]);
-        if (prerelu) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xf[j][ks][e] = xf[j][ks][e] > (h16)0 ? xf[j][ks][e] : (h16)0;
-        }
+        if (prerelu) xf[j][ks] = relu8(xf[j][ks]);
       }
   };
   auto load_w = [&](const h16* base, int qn) {
@@ -787,6 +820,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     mma(1, 0);
   }
   if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
+  TS(3);
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
   if (p.epi.store == VDA_STORE_ROWS) {
@@ -812,63 +846,103 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
       f4 bv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        bv[i] = *reinterpret_cast<const f4*>(e.bias + (ACT == VDA_ACT_GEGLU ? ncl[i & ~1] + (i & 1) * 16 : ncl[i]));
+        bv[i] = PREF ? pbv[i] : *reinterpret_cast<const f4*>(e.bias + (ACT == VDA_ACT_GEGLU ? ncl[i & ~1] + (i & 1) * 16 : ncl[i]));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) acc[i][j] += bv[i];
     }
-    if constexpr (ACT != VDA_ACT_GEGLU) {
+    if constexpr (ACT != VDA_ACT_GEGLU && ROWB) {
       if (e.rowbias) {  // per-row bias (folded positional terms): 4 loads per output row group
+        // (m / rdiv) % rmod by fp32 reciprocals + one integer correction each (m < 2^24: exact)
+        const float inv_div = 1.f / (float)e.rdiv, inv_mod = 1.f / (float)e.rmod;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int m = m0 + wm * 128 + j * 16 + mcol;
-          const long roff = m < p.M ? (long)((m / e.rdiv) % e.rmod) * p.N : 0;
+          int qd = (int)((float)m * inv_div);
+          qd += (m - qd * e.rdiv >= e.rdiv) ? 1 : 0;
+          qd -= (m < qd * e.rdiv) ? 1 : 0;
+          int qm = (int)((float)qd * inv_mod);
+          qm += (qd - qm * e.rmod >= e.rmod) ? 1 : 0;
+          qm -= (qd < qm * e.rmod) ? 1 : 0;
+          const long roff = m < p.M ? (long)(qd - qm * e.rmod) * p.N : 0;
           f4 rb[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) rb[i] = *reinterpret_cast<const f4*>(e.rowbias + roff + ncl[i]);
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[i][j] += rb[i];
+          __builtin_amdgcn_sched_barrier(0);  // keep the loads of row group j+1 after these adds
         }
       }
     }
+    // gamma (layer scale) is normally folded into W and b by the host; the multiply is compiled
+    // only into the has-gamma variant of the loop, and fp32 -> fp16 goes through v_cvt_pk_f16_f32
+    if constexpr (ACT == VDA_ACT_GELU && TAB) {
+      // table GELU in place on the accumulators, 16 values per step: all 16 LDS reads are issued
+      // before the first is consumed (one wait per group instead of one per value)
 #pragma unroll
-    for (int i = 0; i < 4; i += (ACT == VDA_ACT_GEGLU ? 2 : 1)) {
-      const int nl = wn * 64 + i * 16 + nq;  // local W row of this lane's first channel
-      f4 gv = f4{1.f, 1.f, 1.f, 1.f};
-      if (e.gamma)
-        gv = *reinterpret_cast<const f4*>(e.gamma + (ACT == VDA_ACT_GEGLU ? (nok[i] ? (n0 >> 1) + ((wn * 64 + i * 16) >> 1) + nq : 0) : ncl[i]));
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ml = wm * 128 + j * 16 + mcol;
-        f4 v;
-        int col;
-        if constexpr (ACT == VDA_ACT_GEGLU) {
-          const f4 vh = acc[i][j], vg = acc[i + 1][j];
+        for (int j = 0; j < 8; j += 4) {
+          float t[16];
+          int ix[16];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phi_lds) : gelu_erf(vg[r]));
-          v *= gv;
-          col = ((wn * 64 + i * 16) >> 1) + nq;
-        } else {
-          v = acc[i][j];
-          if constexpr (ACT == VDA_ACT_GELU) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = TAB ? gelu_tab(v[r], phi_lds) : gelu_erf(v[r]);
-          } else if constexpr (ACT == VDA_ACT_RELU) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+          for (int k = 0; k < 16; ++k) {
+            const float u = __builtin_amdgcn_fmed3f(fmaf(acc[i][j + k / 4][k % 4], 128.f, 1024.f), 0.f, 2047.9998f);
+            ix[k] = (int)u;
+            t[k] = __builtin_amdgcn_fractf(u);
           }
-          v *= gv;
-          col = nl;
-        }
-        h4 o;
+          float2 ab[16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (h16)v[r];
-        const int u = (col >> 2) ^ (ml & 15);
-        *reinterpret_cast<h4*>(&smem[ml * OW + u * 4]) = o;
-      }
+          for (int k = 0; k < 16; ++k) ab[k] = *reinterpret_cast<const float2*>(phi_lds + 2 * ix[k]);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) acc[i][j + k / 4][k % 4] *= fmaf(t[k], ab[k].y, ab[k].x);
+        }
     }
+    auto phase1 = [&](auto g_tag) {
+      constexpr bool HG = decltype(g_tag)::value;
+#pragma unroll
+      for (int i = 0; i < 4; i += (ACT == VDA_ACT_GEGLU ? 2 : 1)) {
+        const int nl = wn * 64 + i * 16 + nq;  // local W row of this lane's first channel
+        f4 gv = f4{1.f, 1.f, 1.f, 1.f};
+        if constexpr (HG) {
+          if constexpr (PREF) gv = pgv[i];
+          else gv = *reinterpret_cast<const f4*>(e.gamma + (ACT == VDA_ACT_GEGLU ? (nok[i] ? (n0 >> 1) + ((wn * 64 + i * 16) >> 1) + nq : 0) : ncl[i]));
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ml = wm * 128 + j * 16 + mcol;
+          f4 v;
+          int col;
+          if constexpr (ACT == VDA_ACT_GEGLU) {
+            const f4 vh = acc[i][j], vg = acc[i + 1][j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phi_lds) : gelu_erf(vg[r]));
+            col = ((wn * 64 + i * 16) >> 1) + nq;
+          } else {
+            v = acc[i][j];
+            if constexpr (ACT == VDA_ACT_GELU && !TAB) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+            } else if constexpr (ACT == VDA_ACT_RELU) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+            }
+            col = nl;
+          }
+          if constexpr (HG) v *= gv;
+          typedef float f2v __attribute__((ext_vector_type(2)));
+          const h2 lo = __builtin_convertvector(f2v{v[0], v[1]}, h2);
+          const h2 hi = __builtin_convertvector(f2v{v[2], v[3]}, h2);
+          const int u = (col >> 2) ^ (ml & 15);
+          *reinterpret_cast<uint2*>(&smem[ml * OW + u * 4]) = make_uint2(__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi));
+        }
+      }
+    };
+    if (e.gamma) phase1(std::true_type{});
+    else phase1(std::false_type{});
     __syncthreads();
+    TS(4);
     const int nout = (ACT == VDA_ACT_GEGLU) ? (p.N >> 1) : p.N;
     const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
     // Phase 2: thread -> fixed (row0 + RPI * it, 16-byte chunk q).  Every iteration reuses the same
@@ -901,7 +975,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
       unsigned vr1 = 0, sr1 = 0, vr2 = 0, sr2 = 0;
       if constexpr (NR >= 1) { rr1 = rsrc(r1p, r1ld); vr1 = voff(r1ld); sr1 = (unsigned)(RPI * r1ld * 2); }
       if constexpr (NR >= 2) { rr2 = rsrc((const h16*)e.res2, e.ldres2); vr2 = voff(e.ldres2); sr2 = (unsigned)(RPI * e.ldres2 * 2); }
-#pragma unroll
+#pragma unroll 4
       for (int it = 0; it < NIT; ++it) {
         const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
         const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
@@ -914,6 +988,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     if (nres == 0) phase2(std::integral_constant<int, 0>{});
     else if (nres == 1) phase2(std::integral_constant<int, 1>{});
     else phase2(std::integral_constant<int, 2>{});
+    TS(5);
+#ifdef VDA_TS
+    wait_vmcnt<0>();
+    TS(6);
+#endif
     return;
   }
   if constexpr (ACT == VDA_ACT_GEGLU) {
@@ -943,13 +1022,89 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   }
 }
 
+// Persistent: one block per CU walks tiles vb, vb + gridDim.x, ... (virtual block ids keep the
+// XCD-aware tile mapping of a one-tile-per-block grid).  All blocks run equal-length tiles, so left
+// alone every CU would hit its epilogue (HBM store burst) and next prologue (load burst) at the same
+// moment while the MFMAs idle.  When the last round is short (ntiles % grid <= grid / 2), half of
+// the blocks that own one tile fewer start half a tile late (stagger_ticks of the 100 MHz
+// s_memrealtime clock): the bursts of the two halves then overlap the other half's main loop, and
+// the delayed blocks still finish no later than the blocks with the extra tile.
+template <int XR, int WR, bool CONV, int ACT, bool ROWB>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n, int stagger_ticks) {
+  constexpr int BUF = (XR + WR) * 128 * BK;
+  constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0)];
+  const int ntiles = tiles_m * tiles_n;
+  if (stagger_ticks > 0 && (int)blockIdx.x >= ntiles % (int)gridDim.x && ((blockIdx.x >> 3) & 1)) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)stagger_ticks) __builtin_amdgcn_s_sleep(16);
+  }
+  if constexpr (CONV) {  // convs launch one block per tile (phased_sched): no loop-carried state
+    const int vb = blockIdx.x;
+    TS(0);
+    gemm256_tile<XR, WR, CONV, ACT, ROWB>(p, vb, tiles_m, tiles_n, smem);
+    TS(7);
+  } else {
+    for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
+      TS(0);
+      gemm256_tile<XR, WR, CONV, ACT, ROWB>(p, vb, tiles_m, tiles_n, smem);
+      __syncthreads();
+      TS(7);
+    }
+  }
+}
+
 int g_force_tile = -1;  // debug / tuning override (vda_debug_force_tile)
+int g_persist = -1, g_stagger = -1;  // debug overrides (vda_debug_gemm_sched); -1 = automatic
+
+int cu_count() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cached[dev] = n;
+  }
+  return cached[dev];
+}
+
+// grid and start stagger of a phased launch (see gemm256_kernel)
+void phased_sched(int ntiles, int nk, bool conv, int& grid, int& ticks) {
+  const int cus = cu_count();
+  // measured in situ: persistent pays for the dense GEMMs, one block per tile for the convs
+  const int persist = conv ? 0 : (g_persist >= 0 ? g_persist : cus);
+  grid = persist == 0 ? ntiles : std::min(ntiles, persist);
+  ticks = 0;
+  if (g_stagger >= 0) {
+    ticks = g_stagger;
+  } else if (ntiles > grid && ntiles % grid <= grid / 2) {
+    // half a tile: ~1.45 us per 64-deep K step + ~6 us prologue/epilogue at the clock MFMA runs
+    ticks = (int)((nk * 1.45f + 6.f) * 0.5f * 100.f);
+  }
+}
 
 template <int BM, int BN, int NWM, int NWN, int KB, int NS, bool CONV, int ACT>
 void launch_tile(const GemmParams& p, hipStream_t st) {
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   hipLaunchKernelGGL((gemm_kernel<BM, BN, NWM, NWN, KB, NS, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(NWM * NWN * 64),
                      0, st, p, tiles_m, tiles_n);
+}
+
+template <int XR, int WR, bool CONV, int ACT>
+void launch_phased(const GemmParams& p, hipStream_t st) {
+  const int BM = 128 * XR, BN = 128 * WR;
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  int grid, ticks;
+  phased_sched(tiles_m * tiles_n, (p.K + 63) / 64, CONV, grid, ticks);
+  if constexpr (!CONV && ACT == VDA_ACT_NONE) {
+    if (p.epi.rowbias) {
+      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks);
 }
 
 template <bool CONV, int ACT>
@@ -964,8 +1119,10 @@ void launch_act(const GemmParams& p, hipStream_t st) {
                      (!e.res2 || ((uintptr_t)e.res2 % 16 == 0 && e.ldres2 % 8 == 0)) &&
                      (e.act != VDA_ACT_GEGLU || (p.N / 2) % 8 == 0);
     // the phased kernels' dense path needs K % 64 == 0 and 32-bit buffer offsets
-    const bool dense_ok = CONV || (p.K % 64 == 0 && (long)p.M * p.ldx * 2 < (1L << 31) &&
-                                   (long)p.N * p.K * 2 < (1L << 31));
+    // (per-row bias only in the dense, activation-free phased instantiation)
+    const bool dense_ok = (CONV || (p.K % 64 == 0 && (long)p.M * p.ldx * 2 < (1L << 31) &&
+                                    (long)p.N * p.K * 2 < (1L << 31))) &&
+                          (!e.rowbias || (!CONV && ACT == VDA_ACT_NONE));
     if (p.N <= 64 || (p.K <= 256 && p.N < 256)) cfg = 2;
     else if (p.N >= 256 && p.M >= 4096 && dense_ok && (e.store != VDA_STORE_ROWS || a16)) cfg = 4;
     else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 5;
@@ -977,16 +1134,8 @@ void launch_act(const GemmParams& p, hipStream_t st) {
     case 1: launch_tile<256, 128, 4, 2, 32, 4, CONV, ACT>(p, st); break;
     case 2: launch_tile<128, 64, 2, 2, 32, 4, CONV, ACT>(p, st); break;
     case 3: launch_tile<256, 256, 2, 4, 32, 4, CONV, ACT>(p, st); break;
-    case 4: {
-      const int tiles_m = (p.M + 255) / 256, tiles_n = (p.N + 255) / 256;
-      hipLaunchKernelGGL((gemm256_kernel<2, 2, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
-      break;
-    }
-    case 5: {
-      const int tiles_m = (p.M + 511) / 512, tiles_n = (p.N + 127) / 128;
-      hipLaunchKernelGGL((gemm256_kernel<4, 1, CONV, ACT>), dim3(tiles_m * tiles_n), dim3(512), 0, st, p, tiles_m, tiles_n);
-      break;
-    }
+    case 4: launch_phased<2, 2, CONV, ACT>(p, st); break;
+    case 5: launch_phased<4, 1, CONV, ACT>(p, st); break;
     default: launch_tile<128, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
   }
 }
@@ -1137,5 +1286,11 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
 
 extern "C" int vda_debug_force_tile(int32_t cfg) {
   g_force_tile = cfg;
+  return 0;
+}
+
+extern "C" int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger) {
+  g_persist = persist_blocks;
+  g_stagger = stagger;
   return 0;
 }

@@ -279,12 +279,16 @@ class VideoDepthAnything(nn.Module):
             q = _Packed()
             q.n1w, q.n1b = _f(b.norm1.weight).to(dev), _f(b.norm1.bias).to(dev)
             q.qkv_w, q.qkv_b = _h(b.attn.qkv.weight).to(dev), _f(b.attn.qkv.bias).to(dev)
-            q.proj_w, q.proj_b = _h(b.attn.proj.weight).to(dev), _f(b.attn.proj.bias).to(dev)
-            q.ls1 = _f(b.ls1.gamma).to(dev)
+            # LayerScale folded into the projections (gamma * (W h + b) = (gamma W) h + gamma b): the
+            # GEMM epilogue then carries no per-channel multiply (block.py ls1 / ls2)
+            g1 = b.ls1.gamma.detach().float()
+            q.proj_w = _h(b.attn.proj.weight.detach().float() * g1[:, None]).to(dev)
+            q.proj_b = _f(b.attn.proj.bias.detach().float() * g1).to(dev)
             q.n2w, q.n2b = _f(b.norm2.weight).to(dev), _f(b.norm2.bias).to(dev)
             q.fc1_w, q.fc1_b = _h(b.mlp.fc1.weight).to(dev), _f(b.mlp.fc1.bias).to(dev)
-            q.fc2_w, q.fc2_b = _h(b.mlp.fc2.weight).to(dev), _f(b.mlp.fc2.bias).to(dev)
-            q.ls2 = _f(b.ls2.gamma).to(dev)
+            g2 = b.ls2.gamma.detach().float()
+            q.fc2_w = _h(b.mlp.fc2.weight.detach().float() * g2[:, None]).to(dev)
+            q.fc2_b = _f(b.mlp.fc2.bias.detach().float() * g2).to(dev)
             P.blocks.append(q)
         P.nw, P.nb = _f(enc.norm.weight).to(dev), _f(enc.norm.bias).to(dev)
 
@@ -439,10 +443,10 @@ class VideoDepthAnything(nn.Module):
             qkv = ops.gemm(hN, q.qkv_w, bias=q.qkv_b)
             at = ops.spatial_attention(qkv, BT, ntok, P.heads, 64)
             del qkv
-            ops.gemm(at, q.proj_w, bias=q.proj_b, gamma=q.ls1, res=tok, out=tok)
+            ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok)
             hN = ops.layernorm(tok, q.n2w, q.n2b, 1e-6)
             f = ops.gemm(hN, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, tag="enc_fc1")
-            ops.gemm(f, q.fc2_w, bias=q.fc2_b, gamma=q.ls2, res=tok, out=tok)
+            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok)
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
                 feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
