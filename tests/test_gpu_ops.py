@@ -60,6 +60,33 @@ def test_gemm_gelu_ls_residual_rowbias():
     assert rel(y, ref) < 2e-3
 
 
+@pytest.mark.parametrize("K", [64, 128, 192])
+def test_gemm_persistent_tiles(K):
+    """> 256 tiles: the dense phased GEMM walks tiles persistently, staggers half its blocks and
+    streams the next tile's first K step under each epilogue (nk = 1, 2, 3 cover the prologue cases)."""
+    M, N = 20000, 1024
+    x, w, b = rnd(M, K, seed=31), rnd(N, K, scale=K ** -0.5, seed=32), rnd(N, scale=0.1, seed=33)
+    ref = x @ w.t() + b
+    assert rel(ops.gemm(h(x), h(w), bias=f32(b)), ref) < 2e-3
+    assert rel(ops.gemm(h(x), h(w), bias=f32(b), act=ACT_GELU), F.gelu(ref)) < 2e-3
+    res = rnd(M, N, seed=34)
+    r = h(res)
+    ops.gemm(h(x), h(w), bias=f32(b), res=r, out=r)
+    assert rel(r, res + ref) < 2e-3
+    gam = rnd(N, seed=35).abs() + 0.1
+    r2 = h(res)
+    ops.gemm(h(x), h(w), bias=f32(b), gamma=f32(gam), res=r2, res2=h(res), out=r2)
+    assert rel(r2, 2 * res + gam * ref) < 2e-3
+    T, S = 5, 4000
+    rb = rnd(T, N, seed=36)
+    y = ops.gemm(h(x), h(w), rowbias=f32(rb), rdiv=S, rmod=T)
+    assert rel(y, x @ w.t() + rb[(torch.arange(M) // S) % T]) < 2e-3
+    w2, b2 = rnd(2 * N, K, scale=K ** -0.5, seed=37), rnd(2 * N, scale=0.1, seed=38)
+    y = ops.gemm(h(x), h(_geglu_interleave(w2)), bias=f32(_geglu_interleave(b2)), act=ACT_GEGLU)
+    hh, g = (x @ w2.t() + b2).chunk(2, -1)
+    assert rel(y, hh * F.gelu(g)) < 2e-3
+
+
 def test_gemm_geglu():
     M, C = 333, 64
     x = rnd(M, C, seed=10)
