@@ -167,9 +167,9 @@ def _fusion(sd, pre, xs: Sequence[Tensor], size=None):
     return F.conv2d(out, sd[pre + "out_conv.weight"], sd[pre + "out_conv.bias"])
 
 
-def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int, T: int,
-                      skip_tmp_block: bool = False) -> Tensor:
-    """dpt_temporal.py:53-99 (+ dpt.py:47-124, blocks.py).  feats: 4 x [BT, ph*pw, C]."""
+def reassemble(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int) -> List[Tensor]:
+    """DPT reassemble (dpt_temporal.py:55-69 / get_motion_features :101-131, dpt.py:60-90).
+    feats: 4 x [BT, ph*pw, C] -> layer_1..4 NCHW."""
     hp = "head."
     out = []
     for i, t in enumerate(feats):
@@ -182,11 +182,18 @@ def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: i
         elif i == 3:
             x = F.conv2d(x, sd[hp + "resize_layers.3.weight"], sd[hp + "resize_layers.3.bias"], stride=2, padding=1)
         out.append(x)
-    l1, l2, l3, l4 = out
-    mm = hp + "motion_modules."
+    return out
+
+
+def head_from_layers(sd: Dict[str, Tensor], l1: Tensor, l2: Tensor, l3: Tensor, l4: Tensor, ph: int, pw: int,
+                     T: int, skip_tmp_block: bool = False, sel=None) -> Tensor:
+    """dpt_temporal.py:71-99 (clip) and foward_single_image :181-260 (streaming): layer_3/4 carry all
+    T frames; with ``sel`` (frame indices), layer_1/2 carry only the selected frames and path_3 is
+    cut to ``sel`` after motion module 3 (:232-238).  Returns depth [len(sel) or BT, 1, 14ph, 14pw]."""
+    mm = "head.motion_modules."
+    s = "head.scratch."
     l3 = temporal_module(sd, mm + "0.", l3, T)
     l4 = temporal_module(sd, mm + "1.", l4, T)
-    s = hp + "scratch."
     r1 = F.conv2d(l1, sd[s + "layer1_rn.weight"], padding=1)
     r2 = F.conv2d(l2, sd[s + "layer2_rn.weight"], padding=1)
     r3 = F.conv2d(l3, sd[s + "layer3_rn.weight"], padding=1)
@@ -196,6 +203,8 @@ def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: i
         p4 = temporal_module(sd, mm + "2.", p4, T)
     p3 = _fusion(sd, s + "refinenet3.", [p4, r3], size=r2.shape[2:])
     p3 = temporal_module(sd, mm + "3.", p3, T)
+    if sel is not None:
+        p3 = p3[list(sel)]
     p2 = _fusion(sd, s + "refinenet2.", [p3, r2], size=r1.shape[2:])
     p1 = _fusion(sd, s + "refinenet1.", [p2, r1])
     o = F.conv2d(p1, sd[s + "output_conv1.weight"], sd[s + "output_conv1.bias"], padding=1)
@@ -203,6 +212,47 @@ def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: i
     o = F.relu(F.conv2d(o.float(), sd[s + "output_conv2.0.weight"], sd[s + "output_conv2.0.bias"], padding=1))
     o = F.relu(F.conv2d(o, sd[s + "output_conv2.2.weight"], sd[s + "output_conv2.2.bias"]))
     return o
+
+
+def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int, T: int,
+                      skip_tmp_block: bool = False) -> Tensor:
+    """dpt_temporal.py:53-99 (+ dpt.py:47-124, blocks.py).  feats: 4 x [BT, ph*pw, C]."""
+    l1, l2, l3, l4 = reassemble(sd, feats, ph, pw)
+    return head_from_layers(sd, l1, l2, l3, l4, ph, pw, T, skip_tmp_block)
+
+
+class StreamEngine:
+    """The streaming mode's two model calls (video_depth.py:66-88 forward_single_image,
+    dpt_temporal.py:101-131 get_motion_features, :133-260 foward_single_image) in fp32 on the CPU,
+    with the interface ``vda_amd.stream`` drives (features NCHW fp32 here)."""
+
+    def __init__(self, sd: Dict[str, Tensor], enc: str):
+        self.sd = {k: v.float().cpu() for k, v in sd.items()}
+        self.enc = enc
+
+    @torch.no_grad()
+    def motion_features(self, x: Tensor):
+        x = x.float().cpu()
+        ph, pw = x.shape[-2] // PATCH, x.shape[-1] // PATCH
+        return tuple(reassemble(self.sd, encoder_taps(self.sd, self.enc, x), ph, pw))
+
+    @torch.no_grad()
+    def predict(self, x: Tensor, old, pred_idx, T: int, skip_tmp_block: bool = False):
+        x = x.float().cpu()
+        H, W = x.shape[-2:]
+        ph, pw = H // PATCH, W // PATCH
+        new = self.motion_features(x)
+        if pred_idx is not None:
+            l1 = torch.cat([old[0][list(pred_idx)], new[0]], 0)
+            l2 = torch.cat([old[1][list(pred_idx)], new[1]], 0)
+            sel = list(pred_idx) + [T - 1]
+        else:
+            l1, l2, sel = new[0], new[1], [T - 1]
+        l3 = torch.cat([old[2], new[2]], 0)
+        l4 = torch.cat([old[3], new[3]], 0)
+        d = head_from_layers(self.sd, l1, l2, l3, l4, ph, pw, T, skip_tmp_block, sel=sel)
+        d = F.relu(F.interpolate(d, size=(H, W), mode="bilinear", align_corners=True))
+        return d[:, 0], new
 
 
 @torch.no_grad()

@@ -412,29 +412,25 @@ class VideoDepthAnything(nn.Module):
         y = ops.gemm(out.view(-1, Cf), q.out_w, bias=q.out_b).view(BT, h, w, Cf)
         return y, size
 
-    @torch.no_grad()
-    def forward(self, x: torch.Tensor, skip_tmp_block: bool = False) -> torch.Tensor:
+    def _check_input(self, x: torch.Tensor, T: int):
         if not x.is_cuda:
             raise RuntimeError("VideoDepthAnything (MI355X) runs on the GPU only; move the model input to cuda")
-        B, T, Cc, H, W = x.shape
+        Cc, H, W = x.shape[-3:]
         if Cc != 3:
             raise ValueError(f"expected 3 input channels, got {Cc}")
         if H % PATCH or W % PATCH:  # patch_embed.py:73-74
             raise AssertionError(f"Input image size ({H}x{W}) is not a multiple of the patch size {PATCH}")
         if T > self.num_frames:  # PE table length (motion_module.py:198-206)
             raise ValueError(f"clip length {T} exceeds the temporal PE table ({self.num_frames})")
-        dev = x.device
-        P = self._pack(dev)
-        BT = B * T
-        ph, pw = H // PATCH, W // PATCH
-        npt = ph * pw
-        ntok = npt + 1
-        C = P.C
 
-        # ---- DINOv2 encoder (dinov2.py:212-231, :271-321; block.py:104-106)
-        img = x.reshape(BT, 3, H, W).float().contiguous()
-        a = ops.patch_im2col(img, P.Kp)
-        tok = ops.gemm(a, P.patch_w, rowbias=self._token_bias(P, H, W, dev), rdiv=1, rmod=ntok)
+    def _encode(self, P: _Packed, img: torch.Tensor) -> List[torch.Tensor]:
+        """DINOv2 get_intermediate_layers (dinov2.py:212-231, :271-321; block.py:104-106):
+        img [BT, 3, H, W] -> 4 tap maps [BT*np, C] fp16 (final LN applied, cls row dropped)."""
+        BT, _, H, W = img.shape
+        npt = (H // PATCH) * (W // PATCH)
+        ntok = npt + 1
+        a = ops.patch_im2col(img.float().contiguous(), P.Kp)
+        tok = ops.gemm(a, P.patch_w, rowbias=self._token_bias(P, H, W, img.device), rdiv=1, rmod=ntok)
         del a
         taps = self.intermediate_layer_idx[self.encoder]
         feats: List[torch.Tensor] = []
@@ -450,9 +446,11 @@ class VideoDepthAnything(nn.Module):
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
                 feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
-        del tok
+        return feats
 
-        # ---- DPT reassemble (dpt_temporal.py:55-69, dpt.py:60-90)
+    def _reassemble(self, P: _Packed, feats: List[torch.Tensor], BT: int, ph: int, pw: int) -> List[torch.Tensor]:
+        """DPT reassemble (dpt_temporal.py:55-69 == get_motion_features :101-131, dpt.py:60-90):
+        -> layer_1..4 NHWC fp16 [BT, h, w, C]."""
         oc = self.out_channels
         lay = []
         for i, ft in enumerate(feats):
@@ -466,8 +464,15 @@ class VideoDepthAnything(nn.Module):
             else:
                 l = ops.conv2d(p.view(BT, ph, pw, oc[3]), P.rs_w[3], ks=3, stride=2, pad=1, bias=P.rs_b[3])
             lay.append(l)
-        del feats
-        l1, l2, l3, l4 = lay
+        return lay
+
+    def _head(self, P: _Packed, l1, l2, l3, l4, B: int, T: int, ph: int, pw: int, skip_tmp_block: bool,
+              sel: Optional[List[int]] = None) -> torch.Tensor:
+        """Temporal DPT head from the reassembled maps (dpt_temporal.py:71-99).  layer_3/4 carry all
+        B*T frames.  With ``sel`` (streaming, dpt_temporal.py:181-260) layer_1/2 carry only the
+        selected frames and path_3 is cut to them after motion module 3.  -> depth [n, 14ph, 14pw] fp32."""
+        oc = self.out_channels
+        BT = B * T
         h3, w3 = l3.shape[1:3]
         h4, w4 = l4.shape[1:3]
         # temporal modules on layer_3 / layer_4 (dpt_temporal.py:75-76)
@@ -477,7 +482,7 @@ class VideoDepthAnything(nn.Module):
         r2 = ops.conv2d(l2, P.rn[1])
         r3 = ops.conv2d(l3, P.rn[2])
         r4 = ops.conv2d(l4, P.rn[3])
-        del l1, l2, l3, l4, lay
+        del l1, l2, l3, l4
         Fh = self.features
         y, _ = self._fusion(P.ref[4], r4, None, None)
         p4 = ops.upsample_bilinear(y, r3.shape[1], r3.shape[2])
@@ -486,6 +491,8 @@ class VideoDepthAnything(nn.Module):
         y, _ = self._fusion(P.ref[3], p4, r3, None)
         p3 = ops.upsample_bilinear(y, r2.shape[1], r2.shape[2])
         p3 = self._temporal(P.mm[3], p3.view(-1, Fh), B, T, p3.shape[1] * p3.shape[2]).view(p3.shape)
+        if sel is not None:
+            p3 = p3.index_select(0, torch.tensor(sel, dtype=torch.long, device=p3.device))
         y, _ = self._fusion(P.ref[2], p3, r2, None)
         p2 = ops.upsample_bilinear(y, r1.shape[1], r1.shape[2])
         y, _ = self._fusion(P.ref[1], p2, r1, None)  # refinenet1: scale_factor 2
@@ -494,8 +501,94 @@ class VideoDepthAnything(nn.Module):
         o1 = ops.conv2d(ops.upsample_bilinear(y, H1, W1), P.oc1_w, bias=P.oc1_b)
         # output_conv2 with fp32 weights on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
         # the final resize to (H, W) is the identity because H = 14ph, W = 14pw (video_depth.py:63)
-        depth = ops.depth_head(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
+        return ops.depth_head(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, skip_tmp_block: bool = False) -> torch.Tensor:
+        B, T, Cc, H, W = x.shape
+        self._check_input(x, T)
+        P = self._pack(x.device)
+        BT = B * T
+        ph, pw = H // PATCH, W // PATCH
+        feats = self._encode(P, x.reshape(BT, 3, H, W))
+        lay = self._reassemble(P, feats, BT, ph, pw)
+        del feats
+        depth = self._head(P, *lay, B, T, ph, pw, skip_tmp_block)
         return depth.view(B, T, H, W)
+
+    # -- streaming mode (video_depth.py:66-327) ----------------------------------------------
+    @torch.no_grad()
+    def get_motion_features(self, x: torch.Tensor):
+        """Encoder + DPT reassemble of single frames (dpt_temporal.py:101-131 after
+        get_intermediate_layers): x [N, 3, H, W] (or [1, N, 3, H, W]) -> (layer_1..4) NHWC fp16.
+        The reference returns NCHW maps in the autocast dtype; these are the same values laid out
+        for libvda."""
+        if x.dim() == 5:
+            x = x.flatten(0, 1)
+        N, _, H, W = x.shape
+        self._check_input(x, 1)
+        P = self._pack(x.device)
+        return tuple(self._reassemble(P, self._encode(P, x), N, H // PATCH, W // PATCH))
+
+    @torch.no_grad()
+    def forward_single_image(self, x: torch.Tensor, motion_features, pred_depth_idx=None, inference_length: int = 32,
+                             skip_tmp_block: bool = False):
+        """video_depth.py:66-88 + dpt_temporal.py:133-260.  x [1, 1, 3, H, W]; motion_features: the
+        four maps of the ``inference_length - 1`` context frames (NHWC fp16, as from
+        ``get_motion_features``).  Returns (depth [1, P+1, H, W] fp32, the new frame's four maps),
+        P = len(pred_depth_idx) or 0."""
+        B, T1, Cc, H, W = x.shape
+        T = int(inference_length)
+        self._check_input(x, T)
+        if B * T1 != 1:
+            raise ValueError("forward_single_image takes one frame [1, 1, 3, H, W]")
+        P = self._pack(x.device)
+        ph, pw = H // PATCH, W // PATCH
+        new = self._reassemble(P, self._encode(P, x.reshape(1, 3, H, W)), 1, ph, pw)
+        o1, o2, o3, o4 = motion_features
+        if o3.shape[0] + 1 != T or o4.shape[0] + 1 != T:
+            raise ValueError(f"context must hold inference_length - 1 = {T - 1} frames, got {o3.shape[0]}")
+        if pred_depth_idx is not None:
+            pidx = [int(i) for i in pred_depth_idx]
+            if pidx and not all(-o1.shape[0] <= i < o1.shape[0] for i in pidx):
+                bad = next(i for i in pidx if not -o1.shape[0] <= i < o1.shape[0])
+                raise IndexError(f"index {bad} is out of bounds for dimension 0 with size {o1.shape[0]}")
+            it = torch.tensor(pidx, dtype=torch.long, device=x.device)
+            l1 = torch.cat([o1.index_select(0, it), new[0]], 0)
+            l2 = torch.cat([o2.index_select(0, it), new[1]], 0)
+            sel = [i if i >= 0 else i + T for i in pidx] + [T - 1]  # path_3[idx] has T rows (:233)
+        else:
+            l1, l2, sel = new[0], new[1], [T - 1]
+        l3 = torch.cat([o3, new[2]], 0)
+        l4 = torch.cat([o4, new[3]], 0)
+        depth = self._head(P, l1, l2, l3, l4, 1, T, ph, pw, skip_tmp_block, sel=sel)
+        return depth.view(1, len(sel), H, W), tuple(new)
+
+    def infere_single_image(self, frames, target_fps, input_size=518, device="cuda", fp32=False, warmup=True,
+                            inference_length=32, keyframe_list=(0, 12), align_each_new_frame=True,
+                            skip_tmp_block=False):
+        """video_depth.py:91-327 on libvda (see vda_amd.stream).  ``fp32=True`` raises, as for
+        ``infer_video_depth``."""
+        if fp32:
+            raise NotImplementedError("fp32 inference is not implemented on the MI355X path (fp16 compute, fp32 tail)")
+        from .stream import infere_single_image
+        return infere_single_image(_StreamEngine(self), frames, target_fps, input_size=input_size, device=device,
+                                   warmup=warmup, inference_length=inference_length, keyframe_list=keyframe_list,
+                                   align_each_new_frame=align_each_new_frame, skip_tmp_block=skip_tmp_block)
+
+
+class _StreamEngine:
+    """libvda engine for vda_amd.stream: single-frame encode + head over a stored context."""
+
+    def __init__(self, m: VideoDepthAnything):
+        self.m = m
+
+    def motion_features(self, x):
+        return self.m.get_motion_features(x)
+
+    def predict(self, x, old, pred_idx, T, skip_tmp_block=False):
+        d, new = self.m.forward_single_image(x.unsqueeze(0), old, pred_idx, T, skip_tmp_block)
+        return d[0], new
 
 
 def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", fp32=False, skip_tmp_block=False,
