@@ -160,6 +160,24 @@ int vda_depth_head(const void* x, const void* w1, const float* b1, const float* 
                    int32_t C, int32_t Ho, int32_t Wo, void* stream);
 
 /*
+ * Frame preprocessing on the device: uint8 RGB frames [N, h, w, 3] (HWC) -> float [N, 3, H, W]
+ * = (bicubic_resize(frames / 255) - mean[c]) / std[c].  Bicubic a = -0.75, half-pixel centres,
+ * clamped borders, no antialias (cv2.INTER_CUBIC; torch interpolate bicubic align_corners=False).
+ * mean / std: 3 floats each in HOST memory.  Replaces util/transform.py:5-157 (Resize with
+ * keep_aspect_ratio / lower_bound / multiple 14 chooses H, W on the host; NormalizeImage;
+ * PrepareForNet) as video_depth.py:336-361 and :140-146, :209 apply them per frame.
+ */
+int vda_preprocess_frames(const void* frames, float* out, int32_t N, int32_t h, int32_t w, int32_t H,
+                          int32_t W, const float* mean, const float* std, void* stream);
+
+/*
+ * Depth resize to the source frame size: depth [N, H, W] float -> out [N, ho, wo] float, bilinear
+ * align_corners=True.  Replaces video_depth.py:372 (infer_video_depth) and :300 (streaming).
+ */
+int vda_depth_resize(const float* depth, float* out, int32_t N, int32_t H, int32_t W, int32_t ho,
+                     int32_t wo, void* stream);
+
+/*
  * Tuning hook: force the GEMM/conv tile configuration (-1 = automatic; 0 = 128x128/4 waves,
  * 1 = 256x128/8 waves, 2 = 128x64/4 waves, 3 = 256x256/8 waves).  Process-global; for benchmarks.
  */

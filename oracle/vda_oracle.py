@@ -268,6 +268,29 @@ def forward(sd: Dict[str, Tensor], enc: str, x: Tensor, skip_tmp_block: bool = F
     return F.relu(d).squeeze(1).unflatten(0, (B, T))
 
 
+class TorchIO:
+    """Frame preprocessing and depth resize in torch fp32 (the checker for libvda's
+    vda_preprocess_frames / vda_depth_resize).  util/transform.py:5-157 as applied in
+    video_depth.py:336-361 (frame / 255, Resize with INTER_CUBIC, NormalizeImage, PrepareForNet) and
+    video_depth.py:372 / :300 (bilinear align_corners=True back to the frame size).  cv2 is absent,
+    so its INTER_CUBIC is restated as torch bicubic (a = -0.75, align_corners=False): cv2 itself is
+    parity-unpinned."""
+    MEAN = (0.485, 0.456, 0.406)
+    STD = (0.229, 0.224, 0.225)
+
+    @staticmethod
+    def preprocess(frames: Tensor, size) -> Tensor:
+        x = frames.permute(0, 3, 1, 2).float() / 255.0
+        x = F.interpolate(x, size=tuple(size), mode="bicubic", align_corners=False)
+        mean = torch.tensor(TorchIO.MEAN, device=x.device).view(1, 3, 1, 1)
+        std = torch.tensor(TorchIO.STD, device=x.device).view(1, 3, 1, 1)
+        return (x - mean) / std
+
+    @staticmethod
+    def resize_depth(depth: Tensor, size) -> Tensor:
+        return F.interpolate(depth.float().unsqueeze(1), size=tuple(size), mode="bilinear", align_corners=True)[:, 0]
+
+
 def rel_l1(a: Tensor, b: Tensor) -> float:
     """Relative L1 = sum|a-b| / sum|b| (SURVEY.md §8(d) parity metric)."""
     a, b = a.double(), b.double()

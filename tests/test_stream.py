@@ -56,7 +56,7 @@ def test_stream_oracle_matches_reference(case):
     frames, depths, meta = load_stream_golden()
     eng = vda_oracle.StreamEngine(recipe_state_dict("vits"), "vits")
     d, fps = S.infere_single_image(eng, frames, 24, input_size=meta["input_size"], device="cpu",
-                                   **meta["cases"][case])
+                                   io=vda_oracle.TorchIO, **meta["cases"][case])
     assert fps == 24
     assert d.shape == depths[case].shape
     assert rel(d, depths[case]) <= 1e-5
@@ -67,9 +67,10 @@ def test_stream_default_raises_like_reference():
     assert meta["default_raises"].startswith("IndexError")
     eng = vda_oracle.StreamEngine(recipe_state_dict("vits"), "vits")
     with pytest.raises(IndexError):
-        S.infere_single_image(eng, frames[:33], 24, input_size=56, device="cpu")
+        S.infere_single_image(eng, frames[:33], 24, input_size=56, device="cpu", io=vda_oracle.TorchIO)
     with pytest.raises(NotImplementedError):
-        S.infere_single_image(eng, frames[:2], 24, input_size=56, device="cpu", warmup=False)
+        S.infere_single_image(eng, frames[:2], 24, input_size=56, device="cpu", warmup=False,
+                              io=vda_oracle.TorchIO)
 
 
 @pytest.mark.gpu

@@ -65,7 +65,7 @@ def test_video_orchestration_matches_reference_golden():
     frames, depth_ref, meta = load_video_golden()
     sd = recipe_state_dict("vits")
     depth, fps = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
-                                     device="cpu")
+                                     device="cpu", io=vda_oracle.TorchIO)
     assert depth.shape == depth_ref.shape
     err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
     assert err <= 1e-5, err
@@ -86,7 +86,7 @@ def _rank_main(rank, world, port, q):
     frames, _, meta = load_video_golden()
     sd = recipe_state_dict("vits")
     depth, _ = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
-                                   device="cpu", rank=rank, world=world)
+                                   device="cpu", rank=rank, world=world, io=vda_oracle.TorchIO)
     if rank == 0:
         q.put(depth)
     dist.barrier()
@@ -119,3 +119,33 @@ def test_video_on_gpu_matches_reference_golden():
     err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
     print(f"video 57 frames: rel-L1 vs reference = {err:.3e}")
     assert err <= 1e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src,dst", [((48, 64), (56, 70)), ((720, 1280), (518, 924)), ((37, 53), (518, 742)),
+                                     ((518, 518), (518, 518)), ((5, 3), (28, 14))])
+def test_preprocess_kernel_vs_torch(src, dst):
+    """vda_preprocess_frames vs the oracle's torch bicubic + normalise (fp32; down, up, identity, tiny)."""
+    from vda_amd import ops
+    g = torch.Generator().manual_seed(src[0] * 7 + dst[1])
+    fr = torch.randint(0, 256, (3, src[0], src[1], 3), generator=g, dtype=torch.uint8)
+    out = ops.preprocess_frames(fr.cuda(), *dst).cpu()
+    ref = vda_oracle.TorchIO.preprocess(fr.double().to(torch.uint8), dst)
+    assert out.shape == ref.shape == (3, 3) + dst
+    assert (out - ref).abs().max().item() <= 2e-5
+    assert V.DeviceIO.preprocess(fr[:0].cuda(), dst).shape == (0, 3) + dst
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src,dst", [((56, 70), (48, 64)), ((518, 924), (720, 1280)), ((14, 14), (1, 1)),
+                                     ((1, 7), (3, 9))])
+def test_depth_resize_kernel_vs_torch(src, dst):
+    from vda_amd import ops
+    g = torch.Generator().manual_seed(src[1] + dst[0])
+    d = torch.rand(2, *src, generator=g) * 50
+    out = ops.depth_resize(d.cuda(), *dst).cpu()
+    ref = vda_oracle.TorchIO.resize_depth(d, dst)
+    # fp32 source-coordinate rounding (o * (in-1)/(out-1) near o ~ 10^3) moves the blend weight by
+    # ~1e-5, i.e. ~1e-5 of the local depth step: bound it relative to the depth range
+    assert (out - ref).abs().max().item() <= 1e-4 * d.abs().max().item()
+    assert vda_oracle.rel_l1(out, ref) <= 1e-6

@@ -7,6 +7,7 @@ There is deliberately no CPU path: calling an op on a CPU tensor, or without lib
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import torch
@@ -227,4 +228,33 @@ def depth_head(x: Tensor, w1_split: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, 
     rc = _lib.lib().vda_depth_head(x.data_ptr(), w1_split.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
                                    out.data_ptr(), ws.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
     check(rc, "vda_depth_head")
+    return out
+
+
+def preprocess_frames(frames: Tensor, H: int, W: int, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)) -> Tensor:
+    """uint8 frames [N, h, w, 3] (GPU) -> normalised network input [N, 3, H, W] fp32 (bicubic resize)."""
+    _need(frames, torch.uint8, "frames")
+    if frames.dim() != 4 or frames.shape[-1] != 3:
+        raise ValueError(f"frames must be [N, h, w, 3] uint8, got {tuple(frames.shape)}")
+    frames = frames.contiguous()
+    N, h, w, _ = frames.shape
+    out = torch.empty((N, 3, H, W), dtype=torch.float32, device=frames.device)
+    if N == 0:
+        return out
+    m3 = (ctypes.c_float * 3)(*[float(v) for v in mean])
+    s3 = (ctypes.c_float * 3)(*[float(v) for v in std])
+    rc = _lib.lib().vda_preprocess_frames(frames.data_ptr(), out.data_ptr(), N, h, w, H, W, m3, s3, _stream(frames))
+    check(rc, "vda_preprocess_frames")
+    return out
+
+
+def depth_resize(depth: Tensor, ho: int, wo: int) -> Tensor:
+    """depth [N, H, W] fp32 (GPU) -> [N, ho, wo] fp32, bilinear align_corners=True."""
+    _need_contig(depth, torch.float32, "depth")
+    N, H, W = depth.shape
+    out = torch.empty((N, ho, wo), dtype=torch.float32, device=depth.device)
+    if N == 0:
+        return out
+    rc = _lib.lib().vda_depth_resize(depth.data_ptr(), out.data_ptr(), N, H, W, ho, wo, _stream(depth))
+    check(rc, "vda_depth_resize")
     return out

@@ -34,9 +34,8 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
-from .video import compute_scale_and_shift, net_input_size, preprocess
+from .video import DeviceIO, compute_scale_and_shift, net_input_size
 
 
 @dataclass
@@ -107,7 +106,7 @@ class FeatureStore:
 
 def infere_single_image(engine, frames, target_fps, input_size: int = 518, device="cuda", warmup: bool = True,
                         inference_length: int = 32, keyframe_list=(0, 12), align_each_new_frame: bool = True,
-                        skip_tmp_block: bool = False):
+                        skip_tmp_block: bool = False, io=DeviceIO):
     """Per-frame depth for ``frames`` (uint8 [N, h, w, 3]); returns (depth [N', h, w] float32, fps).
 
     video_depth.py:91-327: frames 0..L-2 only fill the feature store; from frame L-1 on every frame
@@ -130,7 +129,7 @@ def infere_single_image(engine, frames, target_fps, input_size: int = 518, devic
     depth_list: List[np.ndarray] = []
     emitted_first = False
     for i in range(n):
-        x = preprocess(frames[i:i + 1].to(dev), size)  # [1, 3, H, W]
+        x = io.preprocess(frames[i:i + 1].to(dev), size)  # [1, 3, H, W]
         if i < L - 1:
             maps = engine.motion_features(x)
             if store is None:
@@ -160,8 +159,7 @@ def infere_single_image(engine, frames, target_fps, input_size: int = 518, devic
             store.put(i, maps)
         else:
             store.shift_in(maps, sch.drop_slot)
-        d = F.interpolate(depth.float().unsqueeze(1), size=(fh, fw), mode="bilinear", align_corners=True)
-        d = d[:, 0].cpu().numpy()
+        d = io.resize_depth(depth, (fh, fw)).cpu().numpy()
         if not align_each_new_frame or not emitted_first:
             depth_list += [d[k] for k in range(d.shape[0])]
             emitted_first = True

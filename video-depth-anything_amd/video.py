@@ -14,8 +14,9 @@ Mirrors ``VideoDepthAnything.infer_video_depth`` (video_depth.py:329-417) and it
 * rank 0 stitches: least-squares scale/shift on keyframe slots {0, 12}, 8-frame linear blend,
   clip at 0 (:379-413).
 
-Preprocessing runs on the GPU with torch bicubic (a=-0.75, the same kernel as cv2.INTER_CUBIC);
-cv2 is not available here, so the resize is parity-unpinned against cv2.
+Preprocessing (bicubic resize + normalise) and the final depth resize run as libvda kernels
+(``DeviceIO``).  cv2 is not available here, so the bicubic resize is pinned against torch bicubic
+(a=-0.75, the same kernel as cv2.INTER_CUBIC), not cv2 itself.
 """
 from __future__ import annotations
 
@@ -24,7 +25,6 @@ from typing import Callable, List, Optional, Sequence
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 INFER_LEN = 32
 OVERLAP = 10
@@ -82,13 +82,22 @@ def net_input_size(height: int, width: int, input_size: int = 518) -> tuple:
     return (_constrain(sh * height, 14, min_val=input_size), _constrain(sw * width, 14, min_val=input_size))
 
 
-def preprocess(frames: torch.Tensor, size: tuple) -> torch.Tensor:
-    """uint8 frames [N, h, w, 3] (any device) -> normalised float [N, 3, H, W] on frames.device."""
-    x = frames.permute(0, 3, 1, 2).float() / 255.0
-    x = F.interpolate(x, size=size, mode="bicubic", align_corners=False)
-    mean = torch.tensor(MEAN, device=x.device).view(1, 3, 1, 1)
-    std = torch.tensor(STD, device=x.device).view(1, 3, 1, 1)
-    return (x - mean) / std
+class DeviceIO:
+    """The per-frame data formats either side of the forward, on libvda kernels:
+    ``preprocess`` uint8 frames [N, h, w, 3] (on the device) -> normalised input [N, 3, H, W] fp32
+    (bicubic resize + ImageNet normalise, vda_preprocess_frames); ``resize_depth`` depth [N, H, W]
+    -> [N, h, w] fp32 (bilinear align_corners=True, vda_depth_resize).  The drivers take any object
+    with these two methods (the tests pass the oracle's torch-CPU restatement, ``TorchIO``)."""
+
+    @staticmethod
+    def preprocess(frames: torch.Tensor, size: tuple) -> torch.Tensor:
+        from . import ops
+        return ops.preprocess_frames(frames, int(size[0]), int(size[1]), MEAN, STD)
+
+    @staticmethod
+    def resize_depth(depth: torch.Tensor, size: tuple) -> torch.Tensor:
+        from . import ops
+        return ops.depth_resize(depth.float().contiguous(), int(size[0]), int(size[1]))
 
 
 # ---- stitching (video_depth.py:375-413, utils/util.py:40-73) --------------------------------
@@ -151,7 +160,8 @@ def stitch(depth_list: List[np.ndarray], n_frames: int) -> np.ndarray:
 
 # ---- driver ---------------------------------------------------------------------------------
 def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, target_fps, input_size: int = 518,
-                      device="cuda", windows_per_batch: int = 1, rank: int = 0, world: int = 1, group=None):
+                      device="cuda", windows_per_batch: int = 1, rank: int = 0, world: int = 1, group=None,
+                      io=DeviceIO):
     """Depth for every frame of ``frames`` (uint8 [N, h, w, 3] numpy or tensor).
 
     ``forward(x[B, 32, 3, H, W]) -> depth[B, 32, H, W]`` is the clip forward (the model, or any
@@ -172,13 +182,12 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
         ks = mine[b0:b0 + windows_per_batch]
         idx = [window_frame_indices(k, n) for k in ks]
         uniq = sorted(set(i for row in idx for i in row))
-        pre = preprocess(frames[uniq].to(dev), size)
+        pre = io.preprocess(frames[uniq].to(dev), size)
         pos = {f: j for j, f in enumerate(uniq)}
         x = torch.stack([pre[[pos[i] for i in row]] for row in idx], 0)
         with torch.no_grad():
             d = forward(x).float()  # [B, 32, H, W]
-        d = F.interpolate(d.flatten(0, 1).unsqueeze(1), size=(h, w), mode="bilinear", align_corners=True)
-        d = d.view(len(ks), INFER_LEN, h, w)
+        d = io.resize_depth(d.flatten(0, 1), (h, w)).view(len(ks), INFER_LEN, h, w)
         for j, k in enumerate(ks):
             out[k] = d[j]
     if world > 1:
