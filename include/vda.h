@@ -178,6 +178,37 @@ int vda_depth_resize(const float* depth, float* out, int32_t N, int32_t H, int32
                      int32_t wo, void* stream);
 
 /*
+ * fp32 mode (infer_video_depth(fp32=True) / autocast off, video_depth.py:366-368): the same ops
+ * with fp32 activations AND fp32 weights, fp32 accumulation on the exact-f32 MFMA
+ * (v_mfma_f32_16x16x4_f32), exact-erf GELU, expf softmax.  Same layouts and epilogue contract as
+ * the fp16 entry points above (vda_epilogue.res / res2 are float here).  Parity tier (i) of
+ * SURVEY.md §8(d).  Requirements: K, ldx, N multiples of 4 (GEGLU: N % 32 == 0); conv Cin, Cout
+ * multiples of 4; spatial attention D == 64; temporal attention T <= 32, D <= 128.
+ */
+int vda_gemm_f32(const float* x, int64_t ldx, const float* w, float* y, int64_t ldy,
+                 int32_t M, int32_t N, int32_t K, const vda_epilogue* epi, void* stream);
+int vda_conv2d_f32(const float* x, const float* w, float* y, int32_t BT, int32_t H, int32_t W,
+                   int32_t Cin, int32_t Cout, int32_t ks, int32_t stride, int32_t pad,
+                   int32_t pre_relu, const vda_epilogue* epi, void* stream);
+int vda_layernorm_f32(const float* x, int64_t ldx, float* y, const float* gamma, const float* beta,
+                      int32_t rows, int32_t C, float eps, int32_t skip_period, void* stream);
+int vda_groupnorm_f32(const float* x, float* y, const float* gamma, const float* beta, int32_t F,
+                      int32_t S, int32_t C, int32_t groups, float eps, void* stream);
+int vda_spatial_attention_f32(const float* qkv, float* out, int32_t B, int32_t N, int32_t H,
+                              int32_t D, float scale, void* stream);
+int vda_temporal_attention_f32(const float* qkv, float* out, int32_t B, int32_t T, int32_t S,
+                               int32_t H, int32_t D, float scale, void* stream);
+int vda_upsample_bilinear_f32(const float* x, float* y, int32_t BT, int32_t H, int32_t W, int32_t C,
+                              int32_t Ho, int32_t Wo, void* stream);
+int vda_patch_im2col_f32(const float* img, float* a, int32_t BT, int32_t H, int32_t W, int32_t Kp,
+                         void* stream);
+/* Depth tail in fp32: bilinear resize into ws_up [BT, Ho, Wo, C], conv3x3(C -> 32, w1 [32, 3, 3, C],
+ * +b1) -> ReLU into ws_mid [BT*Ho*Wo, 32], then 1x1 (w2 [32], +b2) -> ReLU -> depth [BT, Ho, Wo]. */
+int vda_depth_head_f32(const float* x, const float* w1, const float* b1, const float* w2,
+                       const float* b2, float* depth, float* ws_up, float* ws_mid, int32_t BT,
+                       int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo, void* stream);
+
+/*
  * Tuning hook: force the GEMM/conv tile configuration (-1 = automatic; 0 = 128x128/4 waves,
  * 1 = 256x128/8 waves, 2 = 128x64/4 waves, 3 = 256x256/8 waves).  Process-global; for benchmarks.
  */

@@ -8,7 +8,7 @@ Pillow formats; decord when installed), runs ``infer_video_depth`` (or ``infere_
 ``--process_single_image``), and writes the requested outputs (npz ``depths``, float32 TIFF stack,
 source / visualisation videos as .y4m, or .gif/.png/.webp via ``--vis_format``).  ``--synthetic_weights``
 uses the deterministic recipe of vda_amd.weights when no checkpoint is available (this image has none).
-``--fp32`` raises: the accelerated path computes in fp16 with fp32 accumulation.
+``--fp32`` selects the fp32 kernels (the reference's autocast-off path); the default is fp16 compute.
 """
 import argparse
 import os

@@ -17,7 +17,10 @@ LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so"
 EXPORTED = (
     "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
-    "vda_depth_head", "vda_preprocess_frames", "vda_depth_resize", "vda_debug_force_tile", "vda_debug_gemm_sched",
+    "vda_depth_head", "vda_preprocess_frames", "vda_depth_resize",
+    "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
+    "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
+    "vda_debug_force_tile", "vda_debug_gemm_sched",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -63,6 +66,15 @@ def _declare(lib):
         "vda_depth_head": ([P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_preprocess_frames": ([P, P, I, I, I, I, I, POINTER(F), POINTER(F), P], I),
         "vda_depth_resize": ([P, P, I, I, I, I, I, P], I),
+        "vda_gemm_f32": ([P, L, P, P, L, I, I, I, EP, P], I),
+        "vda_conv2d_f32": ([P, P, P, I, I, I, I, I, I, I, I, I, EP, P], I),
+        "vda_layernorm_f32": ([P, L, P, P, P, I, I, F, I, P], I),
+        "vda_groupnorm_f32": ([P, P, P, P, I, I, I, I, F, P], I),
+        "vda_spatial_attention_f32": ([P, P, I, I, I, I, F, P], I),
+        "vda_temporal_attention_f32": ([P, P, I, I, I, I, I, F, P], I),
+        "vda_upsample_bilinear_f32": ([P, P, I, I, I, I, I, I, P], I),
+        "vda_patch_im2col_f32": ([P, P, I, I, I, I, P], I),
+        "vda_depth_head_f32": ([P, P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_debug_force_tile": ([I], I),
         "vda_debug_gemm_sched": ([I, I], I),
     }

@@ -200,16 +200,8 @@ class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
 # ---------------------------------------------------------------------------------------------
 # Packed (kernel-ready) weights
 # ---------------------------------------------------------------------------------------------
-def _h(t):
-    return t.detach().to(torch.float16).contiguous()
-
-
 def _f(t):
     return t.detach().to(torch.float32).contiguous()
-
-
-def _conv_nhwc(w):  # [Cout, Cin, kh, kw] -> [Cout, kh, kw, Cin] fp16
-    return _h(w.detach().permute(0, 2, 3, 1))
 
 
 def _geglu_interleave(t):
@@ -259,16 +251,23 @@ class VideoDepthAnything(nn.Module):
 
     # -- packing ---------------------------------------------------------------------------
     @torch.no_grad()
-    def _pack(self, device) -> _Packed:
-        key = str(device)
+    def _pack(self, device, fp32: bool = False) -> _Packed:
+        """Kernel-ready weights for ``device``: fp16 (the shipped mode) or, with ``fp32``, fp32 copies
+        for the fp32-mode kernels (same layouts, vda.h *_f32)."""
+        key = f"{device}|{'f32' if fp32 else 'f16'}"
         if key in self._packed:
             return self._packed[key]
         dev = torch.device(device)
+        wd = torch.float32 if fp32 else torch.float16
+        _h = lambda t: t.detach().to(wd).contiguous()  # noqa: E731  (weight storage dtype)
+        _conv_nhwc = lambda w: _h(w.detach().permute(0, 2, 3, 1))  # noqa: E731  [Cout, kh, kw, Cin]
         P = _Packed()
+        P.fp32, P.dt = fp32, wd
         enc = self.pretrained
         C = enc.embed_dim
         P.C, P.heads = C, enc.num_heads
-        P.Kp = 640  # 588 = 3*14*14 zero-padded to a multiple of 64 (the LDS-DMA GEMM K step)
+        # 588 = 3*14*14 zero-padded to a multiple of 64 (the LDS-DMA GEMM K step); fp32 GEMM: K % 4
+        P.Kp = 588 if fp32 else 640
         wpe = enc.patch_embed.proj.weight.reshape(C, -1)
         P.patch_w = _h(F.pad(wpe, (0, P.Kp - wpe.shape[1]))).to(dev)
         P.patch_b = _f(enc.patch_embed.proj.bias).to(dev)
@@ -320,9 +319,12 @@ class VideoDepthAnything(nn.Module):
         P.oc1_w, P.oc1_b = _conv_nhwc(s.output_conv1.weight).to(dev), _f(s.output_conv1.bias).to(dev)
         oc2 = s.output_conv2
         w1 = oc2[0].weight.detach().float().permute(0, 2, 3, 1)  # [32, 3, 3, C]
-        w1_hi = w1.half()
-        w1_lo = (w1 - w1_hi.float()).half()  # exact fp16 hi/lo split of the fp32 weights
-        P.oc2_w1 = torch.cat([w1_hi, w1_lo], 0).contiguous().to(dev)  # [64, 3, 3, C] fp16
+        if fp32:
+            P.oc2_w1 = w1.contiguous().to(dev)
+        else:
+            w1_hi = w1.half()
+            w1_lo = (w1 - w1_hi.float()).half()  # exact fp16 hi/lo split of the fp32 weights
+            P.oc2_w1 = torch.cat([w1_hi, w1_lo], 0).contiguous().to(dev)  # [64, 3, 3, C] fp16
         P.oc2_b1 = _f(oc2[0].bias).to(dev)
         P.oc2_w2 = _f(oc2[2].weight.reshape(-1)).to(dev)
         P.oc2_b2 = _f(oc2[2].bias).to(dev)
@@ -429,7 +431,7 @@ class VideoDepthAnything(nn.Module):
         BT, _, H, W = img.shape
         npt = (H // PATCH) * (W // PATCH)
         ntok = npt + 1
-        a = ops.patch_im2col(img.float().contiguous(), P.Kp)
+        a = ops.patch_im2col(img.float().contiguous(), P.Kp, dtype=P.dt)
         tok = ops.gemm(a, P.patch_w, rowbias=self._token_bias(P, H, W, img.device), rdiv=1, rmod=ntok)
         del a
         taps = self.intermediate_layer_idx[self.encoder]
@@ -501,13 +503,17 @@ class VideoDepthAnything(nn.Module):
         o1 = ops.conv2d(ops.upsample_bilinear(y, H1, W1), P.oc1_w, bias=P.oc1_b)
         # output_conv2 with fp32 weights on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
         # the final resize to (H, W) is the identity because H = 14ph, W = 14pw (video_depth.py:63)
+        if P.fp32:
+            return ops.depth_head_f32(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
         return ops.depth_head(o1, P.oc2_w1, P.oc2_b1, P.oc2_w2, P.oc2_b2, ph * PATCH, pw * PATCH)
 
     @torch.no_grad()
-    def forward(self, x: torch.Tensor, skip_tmp_block: bool = False) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, skip_tmp_block: bool = False, *, fp32: bool = False) -> torch.Tensor:
+        """video_depth.py:58-65.  ``fp32=True`` runs every op in fp32 (the reference's forward with
+        autocast off, video_depth.py:366-368); the default is fp16 compute, fp32 accumulation."""
         B, T, Cc, H, W = x.shape
         self._check_input(x, T)
-        P = self._pack(x.device)
+        P = self._pack(x.device, fp32)
         BT = B * T
         ph, pw = H // PATCH, W // PATCH
         feats = self._encode(P, x.reshape(BT, 3, H, W))
@@ -518,7 +524,7 @@ class VideoDepthAnything(nn.Module):
 
     # -- streaming mode (video_depth.py:66-327) ----------------------------------------------
     @torch.no_grad()
-    def get_motion_features(self, x: torch.Tensor):
+    def get_motion_features(self, x: torch.Tensor, *, fp32: bool = False):
         """Encoder + DPT reassemble of single frames (dpt_temporal.py:101-131 after
         get_intermediate_layers): x [N, 3, H, W] (or [1, N, 3, H, W]) -> (layer_1..4) NHWC fp16.
         The reference returns NCHW maps in the autocast dtype; these are the same values laid out
@@ -527,12 +533,12 @@ class VideoDepthAnything(nn.Module):
             x = x.flatten(0, 1)
         N, _, H, W = x.shape
         self._check_input(x, 1)
-        P = self._pack(x.device)
+        P = self._pack(x.device, fp32)
         return tuple(self._reassemble(P, self._encode(P, x), N, H // PATCH, W // PATCH))
 
     @torch.no_grad()
     def forward_single_image(self, x: torch.Tensor, motion_features, pred_depth_idx=None, inference_length: int = 32,
-                             skip_tmp_block: bool = False):
+                             skip_tmp_block: bool = False, *, fp32: bool = False):
         """video_depth.py:66-88 + dpt_temporal.py:133-260.  x [1, 1, 3, H, W]; motion_features: the
         four maps of the ``inference_length - 1`` context frames (NHWC fp16, as from
         ``get_motion_features``).  Returns (depth [1, P+1, H, W] fp32, the new frame's four maps),
@@ -542,7 +548,7 @@ class VideoDepthAnything(nn.Module):
         self._check_input(x, T)
         if B * T1 != 1:
             raise ValueError("forward_single_image takes one frame [1, 1, 3, H, W]")
-        P = self._pack(x.device)
+        P = self._pack(x.device, fp32)
         ph, pw = H // PATCH, W // PATCH
         new = self._reassemble(P, self._encode(P, x.reshape(1, 3, H, W)), 1, ph, pw)
         o1, o2, o3, o4 = motion_features
@@ -567,12 +573,9 @@ class VideoDepthAnything(nn.Module):
     def infere_single_image(self, frames, target_fps, input_size=518, device="cuda", fp32=False, warmup=True,
                             inference_length=32, keyframe_list=(0, 12), align_each_new_frame=True,
                             skip_tmp_block=False):
-        """video_depth.py:91-327 on libvda (see vda_amd.stream).  ``fp32=True`` raises, as for
-        ``infer_video_depth``."""
-        if fp32:
-            raise NotImplementedError("fp32 inference is not implemented on the MI355X path (fp16 compute, fp32 tail)")
+        """video_depth.py:91-327 on libvda (see vda_amd.stream); ``fp32`` selects the fp32 kernels."""
         from .stream import infere_single_image
-        return infere_single_image(_StreamEngine(self), frames, target_fps, input_size=input_size, device=device,
+        return infere_single_image(_StreamEngine(self, fp32), frames, target_fps, input_size=input_size, device=device,
                                    warmup=warmup, inference_length=inference_length, keyframe_list=keyframe_list,
                                    align_each_new_frame=align_each_new_frame, skip_tmp_block=skip_tmp_block)
 
@@ -580,26 +583,24 @@ class VideoDepthAnything(nn.Module):
 class _StreamEngine:
     """libvda engine for vda_amd.stream: single-frame encode + head over a stored context."""
 
-    def __init__(self, m: VideoDepthAnything):
+    def __init__(self, m: VideoDepthAnything, fp32: bool = False):
         self.m = m
+        self.fp32 = fp32
 
     def motion_features(self, x):
-        return self.m.get_motion_features(x)
+        return self.m.get_motion_features(x, fp32=self.fp32)
 
     def predict(self, x, old, pred_idx, T, skip_tmp_block=False):
-        d, new = self.m.forward_single_image(x.unsqueeze(0), old, pred_idx, T, skip_tmp_block)
+        d, new = self.m.forward_single_image(x.unsqueeze(0), old, pred_idx, T, skip_tmp_block, fp32=self.fp32)
         return d[0], new
 
 
 def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", fp32=False, skip_tmp_block=False,
                        windows_per_batch=1, rank=0, world=1, group=None):
-    """video_depth.py:329-417 on the MI355X forward (see vda_amd.video).  ``fp32=True`` is not on
-    the accelerated path (fp16 compute is the shipped mode); it raises instead of silently
-    running something else."""
-    if fp32:
-        raise NotImplementedError("fp32 inference is not implemented on the MI355X path (fp16 compute, fp32 tail)")
+    """video_depth.py:329-417 on the MI355X forward (see vda_amd.video); ``fp32=True`` runs the
+    fp32 kernels (the reference's autocast-off path), the default fp16 compute."""
     from .video import infer_video_depth
-    return infer_video_depth(lambda x: self.forward(x, skip_tmp_block), frames, target_fps, input_size=input_size,
+    return infer_video_depth(lambda x: self.forward(x, skip_tmp_block, fp32=fp32), frames, target_fps, input_size=input_size,
                              device=device, windows_per_batch=windows_per_batch, rank=rank, world=world,
                              group=group)
 

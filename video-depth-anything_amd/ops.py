@@ -60,8 +60,15 @@ def _need_contig(t: Tensor, dtype, name: str):
         raise RuntimeError(f"vda op: {name} must be contiguous")
 
 
+def _dt(x: Tensor):
+    """Activation dtype of an op: fp16 (the shipped mode) or fp32 (fp32 mode, the *_f32 entry points)."""
+    if x.dtype not in (torch.float16, torch.float32):
+        raise RuntimeError(f"vda op: activations must be float16 or float32, got {x.dtype}")
+    return x.dtype
+
+
 def _epilogue(bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None, res2=None,
-              act=ACT_NONE, store=STORE_ROWS, ps=(0, 0, 0, 0)) -> Epilogue:
+              act=ACT_NONE, store=STORE_ROWS, ps=(0, 0, 0, 0), dt=torch.float16) -> Epilogue:
     e = Epilogue()
     for name, t in (("bias", bias), ("rowbias", rowbias), ("gamma", gamma)):
         if t is not None:
@@ -69,11 +76,11 @@ def _epilogue(bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None, res
             setattr(e, name, t.data_ptr())
     e.rdiv, e.rmod = int(rdiv), int(rmod)
     if res is not None:
-        _need(res, torch.float16, "res")
+        _need(res, dt, "res")
         assert res.stride(-1) == 1
         e.res, e.ldres = res.data_ptr(), res.stride(-2) if res.dim() >= 2 else res.shape[-1]
     if res2 is not None:
-        _need(res2, torch.float16, "res2")
+        _need(res2, dt, "res2")
         assert res2.stride(-1) == 1
         e.res2, e.ldres2 = res2.data_ptr(), res2.stride(-2) if res2.dim() >= 2 else res2.shape[-1]
     e.act, e.store = int(act), int(store)
@@ -83,24 +90,26 @@ def _epilogue(bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None, res
 
 def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
          res2=None, act=ACT_NONE, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
-    """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view."""
-    _need(x, torch.float16, "x")
-    _need_contig(w, torch.float16, "w")
+    """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view.
+    fp16 x/w -> vda_gemm; fp32 x/w -> vda_gemm_f32 (fp32 mode)."""
+    dt = _dt(x)
+    _need(x, dt, "x")
+    _need_contig(w, dt, "w")
     assert x.dim() == 2 and x.stride(1) == 1, "x must be a 2-D row-major (possibly row-strided) matrix"
     M, K = x.shape
     N = w.shape[0]
     assert w.shape[1] == K, f"K mismatch {w.shape} vs {x.shape}"
     nout = N // 2 if act == ACT_GEGLU else N
     if out is None:
-        out = torch.empty((M, nout), dtype=torch.float16, device=x.device)
-    assert out.dim() == 2 and out.stride(1) == 1 and out.shape == (M, nout)
-    e = _epilogue(bias, rowbias, rdiv, rmod, gamma, res, res2, act)
+        out = torch.empty((M, nout), dtype=dt, device=x.device)
+    assert out.dim() == 2 and out.stride(1) == 1 and out.shape == (M, nout) and out.dtype == dt
+    e = _epilogue(bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt=dt)
     probe = _PROBE is not None and tag in _PROBE
     if probe:
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-    rc = _lib.lib().vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0),
-                             M, N, K, e, _stream(x))
+    fn = _lib.lib().vda_gemm if dt == torch.float16 else _lib.lib().vda_gemm_f32
+    rc = fn(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), M, N, K, e, _stream(x))
     if probe:
         ev1.record()
         _PROBE[tag].append((ev0, ev1))
@@ -111,14 +120,16 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
 def conv_transpose_ks(x: Tensor, w: Tensor, bias: Tensor, BT: int, h: int, w_: int, k: int) -> Tensor:
     """ConvTranspose2d(kernel = stride = k) as one GEMM with a pixel-shuffle store.
     x [BT*h*w, Cin]; w [k*k*Cout, Cin] packed (i, j, co); bias [k*k*Cout] fp32 -> [BT, h*k, w*k, Cout]."""
-    _need(x, torch.float16, "x")
-    _need_contig(w, torch.float16, "w")
+    dt = _dt(x)
+    _need(x, dt, "x")
+    _need_contig(w, dt, "w")
     M, K = x.shape
     N = w.shape[0]
     cout = N // (k * k)
-    out = torch.empty((BT, h * k, w_ * k, cout), dtype=torch.float16, device=x.device)
-    e = _epilogue(bias=bias, store=STORE_PIXEL_SHUFFLE, ps=(k, cout, h, w_))
-    rc = _lib.lib().vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), N, M, N, K, e, _stream(x))
+    out = torch.empty((BT, h * k, w_ * k, cout), dtype=dt, device=x.device)
+    e = _epilogue(bias=bias, store=STORE_PIXEL_SHUFFLE, ps=(k, cout, h, w_), dt=dt)
+    fn = _lib.lib().vda_gemm if dt == torch.float16 else _lib.lib().vda_gemm_f32
+    rc = fn(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), N, M, N, K, e, _stream(x))
     check(rc, "vda_gemm(pixel-shuffle)")
     return out
 
@@ -127,19 +138,27 @@ def conv2d(x: Tensor, w: Tensor, *, ks=3, stride=1, pad=1, bias=None, pre_relu=F
            res=None, res2=None, up=None) -> Tensor:
     """NHWC conv.  x [BT, H, W, Cin] fp16; w [Cout, ks, ks, Cin] fp16 -> [BT, Ho, Wo, Cout].
     `up=(Hu, Wu)` reads x through a bilinear align_corners=True resize to (Hu, Wu) first."""
-    _need_contig(x, torch.float16, "x")
-    _need_contig(w, torch.float16, "w")
+    dt = _dt(x)
+    _need_contig(x, dt, "x")
+    _need_contig(w, dt, "w")
     BT, H, W, Cin = x.shape
     Cout = w.shape[0]
     assert w.shape[1:] == (ks, ks, Cin), f"weight {tuple(w.shape)} vs Cin={Cin} ks={ks}"
     Hi, Wi = (up if up is not None else (H, W))
     Ho = (Hi + 2 * pad - ks) // stride + 1
     Wo = (Wi + 2 * pad - ks) // stride + 1
-    out = torch.empty((BT, Ho, Wo, Cout), dtype=torch.float16, device=x.device)
+    out = torch.empty((BT, Ho, Wo, Cout), dtype=dt, device=x.device)
     r = res.reshape(-1, Cout) if res is not None else None
     r2 = res2.reshape(-1, Cout) if res2 is not None else None
-    e = _epilogue(bias=bias, res=r, res2=r2, act=act)
+    e = _epilogue(bias=bias, res=r, res2=r2, act=act, dt=dt)
     uh, uw = (up if up is not None else (0, 0))
+    if dt == torch.float32:
+        if up is not None:
+            raise RuntimeError("vda conv2d: the fused-upsample loader is fp16-only")
+        rc = _lib.lib().vda_conv2d_f32(x.data_ptr(), w.data_ptr(), out.data_ptr(), BT, H, W, Cin, Cout, ks, stride,
+                                       pad, int(bool(pre_relu)), e, _stream(x))
+        check(rc, "vda_conv2d_f32")
+        return out
     rc = _lib.lib().vda_conv2d(x.data_ptr(), w.data_ptr(), out.data_ptr(), BT, H, W, Cin, Cout, ks, stride, pad,
                                int(bool(pre_relu)), uh, uw, e, _stream(x))
     check(rc, "vda_conv2d")
@@ -149,15 +168,17 @@ def conv2d(x: Tensor, w: Tensor, *, ks=3, stride=1, pad=1, bias=None, pre_relu=F
 def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period: int = 0,
               rows: Optional[int] = None) -> Tensor:
     """Row LayerNorm of x [R, C] (row-strided ok).  skip_period=np drops each frame's cls row."""
-    _need(x, torch.float16, "x")
+    dt = _dt(x)
+    _need(x, dt, "x")
     _need_contig(gamma, torch.float32, "gamma")
     _need_contig(beta, torch.float32, "beta")
     assert x.dim() == 2 and x.stride(1) == 1
     R, C = x.shape
     if rows is None:
         rows = R if skip_period == 0 else (R // (skip_period + 1)) * skip_period
-    out = torch.empty((rows, C), dtype=torch.float16, device=x.device)
-    rc = _lib.lib().vda_layernorm(x.data_ptr(), x.stride(0), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+    out = torch.empty((rows, C), dtype=dt, device=x.device)
+    fn = _lib.lib().vda_layernorm if dt == torch.float16 else _lib.lib().vda_layernorm_f32
+    rc = fn(x.data_ptr(), x.stride(0), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                                   rows, C, float(eps), int(skip_period), _stream(x))
     check(rc, "vda_layernorm")
     return out
@@ -165,51 +186,64 @@ def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period
 
 def groupnorm(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, eps: float) -> Tensor:
     """GroupNorm on NHWC frames: x [F*S, C] -> same."""
-    _need_contig(x, torch.float16, "x")
+    dt = _dt(x)
+    _need_contig(x, dt, "x")
     R, C = x.shape
     S = R // frames
     out = torch.empty_like(x)
-    rc = _lib.lib().vda_groupnorm(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S, C,
-                                  groups, float(eps), None, _stream(x))
+    if dt == torch.float32:
+        rc = _lib.lib().vda_groupnorm_f32(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S,
+                                          C, groups, float(eps), _stream(x))
+    else:
+        rc = _lib.lib().vda_groupnorm(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S, C,
+                                      groups, float(eps), None, _stream(x))
     check(rc, "vda_groupnorm")
     return out
 
 
 def spatial_attention(qkv: Tensor, B: int, N: int, H: int, D: int = 64) -> Tensor:
-    _need_contig(qkv, torch.float16, "qkv")
+    dt = _dt(qkv)
+    _need_contig(qkv, dt, "qkv")
     assert qkv.shape == (B * N, 3 * H * D)
-    out = torch.empty((B * N, H * D), dtype=torch.float16, device=qkv.device)
-    rc = _lib.lib().vda_spatial_attention(qkv.data_ptr(), out.data_ptr(), B, N, H, D, float(D) ** -0.5,
+    out = torch.empty((B * N, H * D), dtype=dt, device=qkv.device)
+    fn = _lib.lib().vda_spatial_attention if dt == torch.float16 else _lib.lib().vda_spatial_attention_f32
+    rc = fn(qkv.data_ptr(), out.data_ptr(), B, N, H, D, float(D) ** -0.5,
                                           _stream(qkv))
     check(rc, "vda_spatial_attention")
     return out
 
 
 def temporal_attention(qkv: Tensor, B: int, T: int, S: int, H: int, D: int) -> Tensor:
-    _need_contig(qkv, torch.float16, "qkv")
+    dt = _dt(qkv)
+    _need_contig(qkv, dt, "qkv")
     assert qkv.shape == (B * T * S, 3 * H * D)
-    out = torch.empty((B * T * S, H * D), dtype=torch.float16, device=qkv.device)
-    rc = _lib.lib().vda_temporal_attention(qkv.data_ptr(), out.data_ptr(), B, T, S, H, D, float(D) ** -0.5,
+    out = torch.empty((B * T * S, H * D), dtype=dt, device=qkv.device)
+    fn = _lib.lib().vda_temporal_attention if dt == torch.float16 else _lib.lib().vda_temporal_attention_f32
+    rc = fn(qkv.data_ptr(), out.data_ptr(), B, T, S, H, D, float(D) ** -0.5,
                                            _stream(qkv))
     check(rc, "vda_temporal_attention")
     return out
 
 
 def upsample_bilinear(x: Tensor, Ho: int, Wo: int) -> Tensor:
-    _need_contig(x, torch.float16, "x")
+    dt = _dt(x)
+    _need_contig(x, dt, "x")
     BT, H, W, C = x.shape
-    out = torch.empty((BT, Ho, Wo, C), dtype=torch.float16, device=x.device)
-    rc = _lib.lib().vda_upsample_bilinear(x.data_ptr(), out.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
+    out = torch.empty((BT, Ho, Wo, C), dtype=dt, device=x.device)
+    fn = _lib.lib().vda_upsample_bilinear if dt == torch.float16 else _lib.lib().vda_upsample_bilinear_f32
+    rc = fn(x.data_ptr(), out.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
     check(rc, "vda_upsample_bilinear")
     return out
 
 
-def patch_im2col(img: Tensor, Kp: int) -> Tensor:
+def patch_im2col(img: Tensor, Kp: int, dtype=torch.float16) -> Tensor:
+    """images [BT, 3, H, W] fp32 -> im2col rows [BT*(1+np), Kp] of ``dtype`` (fp16, or fp32 for fp32 mode)."""
     _need_contig(img, torch.float32, "img")
     BT, _, H, W = img.shape
     np_ = (H // 14) * (W // 14)
-    out = torch.empty((BT * (1 + np_), Kp), dtype=torch.float16, device=img.device)
-    rc = _lib.lib().vda_patch_im2col(img.data_ptr(), out.data_ptr(), BT, H, W, Kp, _stream(img))
+    out = torch.empty((BT * (1 + np_), Kp), dtype=dtype, device=img.device)
+    fn = _lib.lib().vda_patch_im2col if dtype == torch.float16 else _lib.lib().vda_patch_im2col_f32
+    rc = fn(img.data_ptr(), out.data_ptr(), BT, H, W, Kp, _stream(img))
     check(rc, "vda_patch_im2col")
     return out
 
@@ -257,4 +291,20 @@ def depth_resize(depth: Tensor, ho: int, wo: int) -> Tensor:
         return out
     rc = _lib.lib().vda_depth_resize(depth.data_ptr(), out.data_ptr(), N, H, W, ho, wo, _stream(depth))
     check(rc, "vda_depth_resize")
+    return out
+
+
+def depth_head_f32(x: Tensor, w1: Tensor, b1: Tensor, w2: Tensor, b2: Tensor, Ho: int, Wo: int) -> Tensor:
+    """fp32-mode depth tail: x [BT, H, W, C] fp32; w1 [32, 3, 3, C] fp32 -> depth [BT, Ho, Wo] fp32."""
+    _need_contig(x, torch.float32, "x")
+    for n, t in (("w1", w1), ("b1", b1), ("w2", w2), ("b2", b2)):
+        _need_contig(t, torch.float32, n)
+    BT, H, W, C = x.shape
+    assert w1.shape == (32, 3, 3, C)
+    up = torch.empty((BT, Ho, Wo, C), dtype=torch.float32, device=x.device)
+    mid = torch.empty((BT * Ho * Wo, 32), dtype=torch.float32, device=x.device)
+    out = torch.empty((BT, Ho, Wo), dtype=torch.float32, device=x.device)
+    rc = _lib.lib().vda_depth_head_f32(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(),
+                                       out.data_ptr(), up.data_ptr(), mid.data_ptr(), BT, H, W, C, Ho, Wo, _stream(x))
+    check(rc, "vda_depth_head_f32")
     return out
