@@ -105,11 +105,14 @@ int vda_layernorm(const void* x, int64_t ldx, void* y, const float* gamma, const
 
 /*
  * GroupNorm over NHWC frames: X [F, S, C] half -> Y [F, S, C] half, `groups` groups of C/groups
- * channels, statistics over (S x C/groups) in fp32.  `ws` is a float workspace of >= 2*F*groups
- * entries.  Replaces motion_module.py:116 (GroupNorm(32, eps 1e-6)).
+ * channels, statistics over (S x C/groups) in fp32.  `ws`: a float workspace of
+ * vda_groupnorm_workspace(F, S, C, groups) entries enables the three-pass coalesced path
+ * (per-chunk partial sums around a per-group shift, finalize, apply; deterministic); NULL runs the
+ * one-block-per-(frame, group) kernel.  Replaces motion_module.py:116 (GroupNorm(32, eps 1e-6)).
  */
 int vda_groupnorm(const void* x, void* y, const float* gamma, const float* beta, int32_t F,
                   int32_t S, int32_t C, int32_t groups, float eps, float* ws, void* stream);
+int64_t vda_groupnorm_workspace(int32_t F, int32_t S, int32_t C, int32_t groups);
 
 /*
  * Spatial multi-head self-attention (flash / online softmax, fp16 MFMA, fp32 softmax).

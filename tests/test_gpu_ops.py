@@ -175,14 +175,27 @@ def test_layernorm_skip_cls():
     assert rel(y, ref) < 2e-3
 
 
-@pytest.mark.parametrize("C,S", [(1024, 50), (256, 70), (384, 33), (64, 90)])
+@pytest.mark.parametrize("C,S", [(1024, 50), (256, 70), (384, 33), (64, 90), (192, 300), (256, 5476)])
 def test_groupnorm(C, S):
+    """Both GroupNorm paths: the workspace (three-pass, row-coalesced) path ops uses, and the
+    one-block-per-group path the C ABI runs with ws = NULL; a large common offset checks that the
+    shifted one-pass variance does not cancel."""
     Fr = 3
     x = rnd(Fr, S, C, seed=36) + 0.3
+    x[1] += 40.0
     g, b = rnd(C, seed=37) * 0.1 + 1, rnd(C, seed=38) * 0.1
-    y = ops.groupnorm(h(x.reshape(-1, C)), f32(g), f32(b), Fr, 32, 1e-6)
-    ref = F.group_norm(x.permute(0, 2, 1), 32, g, b, eps=1e-6).permute(0, 2, 1).reshape(-1, C)
+    xh = h(x.reshape(-1, C))
+    y = ops.groupnorm(xh, f32(g), f32(b), Fr, 32, 1e-6)
+    ref = F.group_norm(xh.float().cpu().view(Fr, S, C).permute(0, 2, 1), 32, g, b, eps=1e-6)
+    ref = ref.permute(0, 2, 1).reshape(-1, C)
     assert rel(y, ref) < 2e-3
+    assert torch.equal(y, ops.groupnorm(xh, f32(g), f32(b), Fr, 32, 1e-6))  # deterministic
+    y0 = torch.empty_like(xh)
+    gd, bd = f32(g), f32(b)  # keep the device copies alive across the launch
+    rc = vda_amd._libvda().vda_groupnorm(xh.data_ptr(), y0.data_ptr(), gd.data_ptr(), bd.data_ptr(), Fr, S,
+                                         C, 32, 1e-6, None, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    assert rel(y0, ref) < 2e-3
 
 
 @pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1)])

@@ -148,4 +148,4 @@ def test_depth_resize_kernel_vs_torch(src, dst):
     # fp32 source-coordinate rounding (o * (in-1)/(out-1) near o ~ 10^3) moves the blend weight by
     # ~1e-5, i.e. ~1e-5 of the local depth step: bound it relative to the depth range
     assert (out - ref).abs().max().item() <= 1e-4 * d.abs().max().item()
-    assert vda_oracle.rel_l1(out, ref) <= 1e-6
+    assert vda_oracle.rel_l1(out, ref) <= 2e-5  # white-noise depth: the worst case for weight rounding

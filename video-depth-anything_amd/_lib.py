@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so"
 
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
-    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm",
+    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm", "vda_groupnorm_workspace",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
     "vda_depth_head", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
@@ -59,6 +59,7 @@ def _declare(lib):
         "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P], I),
         "vda_layernorm": ([P, L, P, P, P, I, I, F, I, P], I),
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
+        "vda_groupnorm_workspace": ([I, I, I, I], L),
         "vda_spatial_attention": ([P, P, I, I, I, I, F, P], I),
         "vda_temporal_attention": ([P, P, I, I, I, I, I, F, P], I),
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),

@@ -112,6 +112,125 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(const h16* __restrict__ 
   }
 }
 
+// GroupNorm, three coalesced passes over [F, S, C] (used when the caller passes a workspace):
+//   gn_partial:  block (frame, chunk of GN_ROWS rows) reads whole rows (16 B per thread) and writes
+//                per-channel partial sums of d and d^2, d = x - shift_g (shift_g = the group's first
+//                value of the frame, so the one-pass variance does not cancel);
+//   gn_finalize: per (frame, group) mean and rstd from the partials, fixed summation order;
+//   gn_apply:    y = (x - mean) * rstd * gamma + beta, same row-chunk grid.
+// Deterministic (no atomics).  The per-(frame, group) kernel above reads strided 16-B slivers of
+// every row three times; these read each row once per pass with full-row coalescing.
+constexpr int GN_ROWS = 128;
+
+__device__ __forceinline__ void gn_layout(int C, int& cpr, int& rpi) {
+  cpr = C >> 3;          // 8-channel chunks per row
+  rpi = 256 / cpr;       // rows per block iteration
+}
+
+__global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__ x, float* __restrict__ part, int S, int C,
+                                                         int groups, int nchunk) {
+  __shared__ float red[256 * 16];  // [thread][sum d x8 | sum d^2 x8] (16 KB)
+  const int f = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  int cpr, rpi;
+  gn_layout(C, cpr, rpi);
+  const int tid = threadIdx.x;
+  const int cc = tid % cpr, r0 = tid / cpr;
+  const int cg = C / groups;
+  const h16* fx = x + (long)f * S * C;
+  float sh[8], s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[j] = (float)fx[((cc * 8 + j) / cg) * cg];
+    s1[j] = 0.f;
+    s2[j] = 0.f;
+  }
+  if (r0 < rpi) {
+    const int rend = min(S, (ch + 1) * GN_ROWS);
+    for (int r = ch * GN_ROWS + r0; r < rend; r += rpi) {
+      const h8 v = __builtin_bit_cast(h8, ldg16(fx + (long)r * C + cc * 8));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = (float)v[j] - sh[j];
+        s1[j] += d;
+        s2[j] = fmaf(d, d, s2[j]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[tid * 16 + j] = s1[j];
+    red[tid * 16 + 8 + j] = s2[j];
+  }
+  __syncthreads();
+  if (tid < cpr) {  // fold the rpi row-lanes of chunk column tid, fixed order
+    float a1[8], a2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { a1[j] = 0.f; a2[j] = 0.f; }
+    for (int q = 0; q < rpi; ++q) {
+      const float* rr = &red[(q * cpr + tid) * 16];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { a1[j] += rr[j]; a2[j] += rr[8 + j]; }
+    }
+    float* out = part + ((long)(f * nchunk + ch) * C + tid * 8) * 2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { out[2 * j] = a1[j]; out[2 * j + 1] = a2[j]; }
+  }
+}
+
+__global__ __launch_bounds__(64) void gn_finalize_kernel(const h16* __restrict__ x, const float* __restrict__ part,
+                                                         float* __restrict__ stats, int S, int C, int groups, int nchunk,
+                                                         float eps) {
+  const int f = blockIdx.x / groups, g = blockIdx.x % groups;
+  const int cg = C / groups;
+  const int lane = threadIdx.x;
+  float a1 = 0.f, a2 = 0.f;
+  const int n = nchunk * cg;
+  for (int i = lane; i < n; i += 64) {
+    const int chn = i / cg, c = g * cg + (i - chn * cg);
+    const float* p = part + ((long)(f * nchunk + chn) * C + c) * 2;
+    a1 += p[0];
+    a2 += p[1];
+  }
+  a1 = wave_sum(a1);
+  a2 = wave_sum(a2);
+  if (lane == 0) {
+    const float cnt = (float)S * (float)cg;
+    const float md = a1 / cnt;
+    const float var = fmaxf(a2 / cnt - md * md, 0.f);
+    stats[(f * groups + g) * 2] = (float)x[(long)f * S * C + g * cg] + md;
+    stats[(f * groups + g) * 2 + 1] = rsqrtf(var + eps);
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x, h16* __restrict__ y,
+                                                       const float* __restrict__ stats, const float* __restrict__ gam,
+                                                       const float* __restrict__ bet, int S, int C, int groups, int nchunk) {
+  const int f = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+  int cpr, rpi;
+  gn_layout(C, cpr, rpi);
+  const int tid = threadIdx.x;
+  const int cc = tid % cpr, r0 = tid / cpr;
+  if (r0 >= rpi) return;
+  const int cg = C / groups;
+  float sc[8], of[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = cc * 8 + j, g = c / cg;
+    const float mean = stats[(f * groups + g) * 2], rstd = stats[(f * groups + g) * 2 + 1];
+    sc[j] = rstd * gam[c];
+    of[j] = bet[c] - mean * sc[j];
+  }
+  const long fo = (long)f * S * C;
+  const int rend = min(S, (ch + 1) * GN_ROWS);
+  for (int r = ch * GN_ROWS + r0; r < rend; r += rpi) {
+    const h8 v = __builtin_bit_cast(h8, ldg16(x + fo + (long)r * C + cc * 8));
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (h16)fmaf((float)v[j], sc[j], of[j]);
+    stg16(y + fo + (long)r * C + cc * 8, __builtin_bit_cast(uint4, o));
+  }
+}
+
 }  // namespace
 
 extern "C" int vda_layernorm(const void* x, int64_t ldx, void* y, const float* gamma, const float* beta,
@@ -126,14 +245,30 @@ extern "C" int vda_layernorm(const void* x, int64_t ldx, void* y, const float* g
   return 0;
 }
 
+extern "C" int64_t vda_groupnorm_workspace(int32_t F, int32_t S, int32_t C, int32_t groups) {
+  if (F <= 0 || S <= 0 || C <= 0 || groups <= 0) return 0;
+  const long nchunk = (S + GN_ROWS - 1) / GN_ROWS;
+  return (int64_t)(2L * F * nchunk * C + 2L * F * groups);
+}
+
 extern "C" int vda_groupnorm(const void* x, void* y, const float* gamma, const float* beta, int32_t F,
                              int32_t S, int32_t C, int32_t groups, float eps, float* ws, void* stream) {
-  (void)ws;
   VDA_CHECK_ARG(x && y && gamma && beta, "null pointer");
   VDA_CHECK_ARG(F > 0 && S > 0 && groups > 0 && C % groups == 0, "C must be divisible by groups");
   const int cg = C / groups;
   VDA_CHECK_ARG(cg % 2 == 0, "channels per group must be even");
   hipStream_t st = (hipStream_t)stream;
+  if (ws && C % 8 == 0 && C <= 2048) {
+    const int nchunk = (S + GN_ROWS - 1) / GN_ROWS;
+    float* stats = ws + 2L * F * nchunk * C;
+    hipLaunchKernelGGL(gn_partial_kernel, dim3(F * nchunk), dim3(256), 0, st, (const h16*)x, ws, S, C, groups, nchunk);
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(F * groups), dim3(64), 0, st, (const h16*)x, (const float*)ws, stats, S,
+                       C, groups, nchunk, eps);
+    hipLaunchKernelGGL(gn_apply_kernel, dim3(F * nchunk), dim3(256), 0, st, (const h16*)x, (h16*)y, (const float*)stats,
+                       gamma, beta, S, C, groups, nchunk);
+    VDA_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid(F * groups);
   if (cg % 8 == 0)
     hipLaunchKernelGGL(groupnorm_kernel<8>, grid, dim3(256), 0, st, (const h16*)x, (h16*)y, gamma, beta, S, C, groups, eps);

@@ -195,8 +195,10 @@ def groupnorm(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, 
         rc = _lib.lib().vda_groupnorm_f32(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S,
                                           C, groups, float(eps), _stream(x))
     else:
+        nws = _lib.lib().vda_groupnorm_workspace(frames, S, C, groups)
+        ws = torch.empty((nws,), dtype=torch.float32, device=x.device)
         rc = _lib.lib().vda_groupnorm(x.data_ptr(), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(), frames, S, C,
-                                      groups, float(eps), None, _stream(x))
+                                      groups, float(eps), ws.data_ptr(), _stream(x))
     check(rc, "vda_groupnorm")
     return out
 
