@@ -75,3 +75,22 @@ def test_model_refuses_cpu_input():
     m = vda_amd.VideoDepthAnything.from_config("vits", device="meta")
     with pytest.raises(RuntimeError, match="GPU only"):
         m(torch.zeros(1, 2, 3, 28, 28))
+
+
+def test_torch_ops_registered_meta_shapes_and_no_cpu_kernel():
+    """torch.ops.vda.* exist, trace shapes under the Meta key, and have no CPU kernel (no fallback)."""
+    import torch
+    import vda_amd.torch_ops  # noqa: F401
+    x = torch.empty(100, 64, device="meta", dtype=torch.float16)
+    w = torch.empty(96, 64, device="meta", dtype=torch.float16)
+    assert torch.ops.vda.gemm(x, w, None, None, 1, 1, None, None, None, 0).shape == (100, 96)
+    assert torch.ops.vda.gemm(x, w, None, None, 1, 1, None, None, None, 2).shape == (100, 48)
+    m = torch.empty(2, 10, 12, 64, device="meta", dtype=torch.float16)
+    wc = torch.empty(32, 3, 3, 64, device="meta", dtype=torch.float16)
+    assert torch.ops.vda.conv2d(m, wc, 3, 2, 1, None, False, 0, None, None).shape == (2, 5, 6, 32)
+    assert torch.ops.vda.layernorm(x, x.new_empty(64, dtype=torch.float32), x.new_empty(64, dtype=torch.float32),
+                                   1e-6, 9).shape == (90, 64)
+    img = torch.empty(2, 3, 28, 42, device="meta")
+    assert torch.ops.vda.patch_im2col(img, 640, False).shape == (2 * 7, 640)
+    with pytest.raises(NotImplementedError):
+        torch.ops.vda.upsample_bilinear(torch.zeros(1, 2, 2, 8, dtype=torch.float16), 4, 4)

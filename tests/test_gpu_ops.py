@@ -264,3 +264,14 @@ def test_depth_head_fp32():
 def test_ops_reject_cpu_tensors():
     with pytest.raises(RuntimeError):
         ops.gemm(torch.zeros(4, 8, dtype=torch.float16), torch.zeros(4, 8, dtype=torch.float16))
+
+
+def test_torch_ops_dispatch_to_libvda():
+    """torch.ops.vda.* (CUDA key) run the same kernels as ops.* (bitwise)."""
+    import vda_amd.torch_ops  # noqa: F401
+    x, w, b = rnd(300, 128, seed=70), rnd(256, 128, scale=128 ** -0.5, seed=71), rnd(256, scale=0.1, seed=72)
+    y0 = ops.gemm(h(x), h(w), bias=f32(b), act=ACT_GELU)
+    y1 = torch.ops.vda.gemm(h(x), h(w), f32(b), None, 1, 1, None, None, None, ACT_GELU)
+    assert torch.equal(y0, y1)
+    m = h(rnd(2, 9, 11, 64, seed=73))
+    assert torch.equal(torch.ops.vda.upsample_bilinear(m, 17, 21), ops.upsample_bilinear(m, 17, 21))
