@@ -244,21 +244,33 @@ def test_patch_embed_im2col_gemm():
     assert rel(y[:, 1:], ref) < 2e-3
 
 
-def test_depth_head_fp32():
-    BT, C, Hin, Win, Ho, Wo = 2, 32, 16, 20, 28, 42
+@pytest.mark.parametrize("C,Hin,Win,Ho,Wo,BT", [(32, 16, 20, 28, 42, 2), (128, 20, 24, 37, 51, 2), (64, 9, 9, 16, 16, 1),
+                                                 (128, 37, 37, 70, 70, 3), (96, 10, 12, 20, 22, 1)])
+def test_depth_head_fp32(C, Hin, Win, Ho, Wo, BT):
+    """Depth tail: the halo-tiled kernel (C = 32 or C % 64 == 0; tile edges 16 with partial tiles here),
+    the implicit-GEMM kernel (other C, and the tuning override) vs torch fp32."""
     x = rnd(BT, C, Hin, Win, seed=45)
-    w1, b1 = rnd(32, C, 3, 3, scale=(9 * C) ** -0.5, seed=46), rnd(32, scale=0.1, seed=47)
+    b1 = rnd(32, scale=0.1, seed=47)
     w2, b2 = rnd(1, 32, 1, 1, seed=48).abs() * 0.2, torch.tensor([0.05])
     w1 = torch.randn(32, C, 3, 3, generator=torch.Generator().manual_seed(46)) * (9 * C) ** -0.5  # full fp32 weights
-    up = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=True)
+    xh = h(x.permute(0, 2, 3, 1))
+    up = F.interpolate(xh.float().cpu().permute(0, 3, 1, 2), size=(Ho, Wo), mode="bilinear", align_corners=True)
+    up = up.half().float()  # the resized map is stored in fp16 (as the reference's autocast interpolate does)
     ref = F.relu(F.conv2d(F.relu(F.conv2d(up, w1, b1, padding=1)), w2, b2))[:, 0]
     wn = w1.permute(0, 2, 3, 1)
-    split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0)
-    y = ops.depth_head(h(x.permute(0, 2, 3, 1)), split.to(DEV).contiguous(), f32(b1), f32(w2.reshape(-1)), f32(b2),
-                       Ho, Wo)
-    # the resized map is stored in fp16 (as the reference's autocast interpolate does); the conv
-    # itself keeps the fp32 weights (hi/lo split) with fp32 accumulation
-    assert rel(y, ref) < 5e-4
+    split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0).to(DEV).contiguous()
+    args = (split, f32(b1), f32(w2.reshape(-1)), f32(b2), Ho, Wo)
+    y = ops.depth_head(xh, *args)
+    # the conv keeps the fp32 weights as hi + lo fp16 halves (22 of 24 mantissa bits) with fp32
+    # accumulation: agreement at ~1e-6
+    assert rel(y, ref) < 1e-5
+    lib = vda_amd._libvda()
+    lib.vda_debug_force_tile(13)  # the implicit-GEMM depth kernel
+    try:
+        y_old = ops.depth_head(xh, *args)
+    finally:
+        lib.vda_debug_force_tile(-1)
+    assert rel(y_old, ref) < 1e-5
 
 
 def test_ops_reject_cpu_tensors():

@@ -1239,6 +1239,9 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   return launch<true>(p, (hipStream_t)stream);
 }
 
+int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
+                   int BT, int H, int W, int C, hipStream_t st);
+
 extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                               float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho,
                               int32_t Wo, void* stream) {
@@ -1250,7 +1253,12 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   //    reference's autocast interpolate (dpt_temporal.py:92-94)
   int rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
   if (rc) return rc;
-  // 2) 3x3 conv C -> 32 with split-fp16 weights + fused ReLU / 1x1 / ReLU epilogue
+  // 2) 3x3 conv C -> 32 with split-fp16 weights + fused ReLU / 1x1 / ReLU epilogue: the halo-tiled
+  //    kernel (vda_depth.hip) unless a tuning override asks for the implicit-GEMM one
+  if (g_force_tile < 10) {
+    rc = vda_depth_halo(ws, w1, b1, w2, b2, depth, BT, Ho, Wo, C, st);
+    if (rc != 1) return rc;
+  }
   GemmParams p{};
   p.x = (const h16*)ws; p.w = (const h16*)w1; p.y = (h16*)depth;
   p.H = Ho; p.W = Wo; p.Cin = C; p.ks = 3; p.stride = 1; p.pad = 1; p.pre_relu = 0;
