@@ -287,3 +287,23 @@ def test_torch_ops_dispatch_to_libvda():
     assert torch.equal(y0, y1)
     m = h(rnd(2, 9, 11, 64, seed=73))
     assert torch.equal(torch.ops.vda.upsample_bilinear(m, 17, 21), ops.upsample_bilinear(m, 17, 21))
+
+
+@pytest.mark.parametrize("Cin,H,W,relu", [(256, 130, 140, False), (128, 129, 131, True)])
+def test_conv3x3_halo_cout128(Cin, H, W, relu):
+    """3x3 convs with 128 outputs on maps >= 128^2 run the halo-tiled kernel (output_conv1, dpt.py:117);
+    vs torch fp32 and vs the implicit-GEMM conv (tuning override)."""
+    x = rnd(2, Cin, H, W, seed=80)
+    w, b = rnd(128, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=81), rnd(128, scale=0.1, seed=82)
+    ref = F.conv2d(x, w, b, padding=1)
+    ref = (F.relu(ref) if relu else ref).permute(0, 2, 3, 1)
+    xh, wh = h(x.permute(0, 2, 3, 1)), h(w.permute(0, 2, 3, 1))
+    y = ops.conv2d(xh, wh, bias=f32(b), act=ACT_RELU if relu else 0)
+    assert rel(y, ref) < 2e-3
+    lib = vda_amd._libvda()
+    lib.vda_debug_force_tile(3)
+    try:
+        y2 = ops.conv2d(xh, wh, bias=f32(b), act=ACT_RELU if relu else 0)
+    finally:
+        lib.vda_debug_force_tile(-1)
+    assert rel(y, y2) < 1e-3

@@ -47,17 +47,23 @@ __device__ __forceinline__ int w_pos(int n, int cd) {
   return cd ^ ((n >> 1) & (CPX - 1));
 }
 
-template <int SLAB>
-__global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
-                                                         const float* __restrict__ b1, const float* __restrict__ w2,
-                                                         const float* __restrict__ b2, float* __restrict__ depth,
-                                                         int H, int W, int C, int tiles_x, int tiles_y, int ntiles) {
+// DEPTH: the depth tail (64 weight rows = 32 hi + 32 lo, wave n-blocks {ng, ng+2}, ReLU/1x1/ReLU epilogue
+// to fp32 depth).  !DEPTH: a plain 3x3 conv with NROW output channels (wave n-blocks ng*NB4 .. +NB4-1,
+// epilogue +bias [ReLU] -> fp16 NHWC).  TPS taps per pipeline step (3 = one kernel row, or 1).
+template <int SLAB, int NROW, int TPS, bool DEPTH>
+__global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
+                                                        const float* __restrict__ b1, const float* __restrict__ w2,
+                                                        const float* __restrict__ b2, float* __restrict__ depth,
+                                                        h16* __restrict__ yout, int relu_out,
+                                                        int H, int W, int C, int tiles_x, int tiles_y, int ntiles) {
+  static_assert(!DEPTH || NROW == 64, "depth tail: 64 weight rows");
+  constexpr int NB = NROW / 32;                          // n-blocks per wave (2 for the depth tail)
   constexpr int CPX = SLAB / 8;                          // 16-B chunks per pixel per slab
   constexpr int PSLOT = DNPIX * CPX;                     // 16-B slots of one patch slab
   constexpr int PP = (PSLOT + 63) / 64;                  // 1-KiB DMA pieces per slab
   constexpr int PBUF = PP * 64 * 8;                      // halfs per patch ring slot
-  constexpr int WROW = 3 * CPX;                          // slots per weight row: 3 taps (one kernel row)
-  constexpr int WSLOT = 64 * WROW;                       // 16-B slots of one weight step
+  constexpr int WROW = TPS * CPX;                        // slots per weight row per step
+  constexpr int WSLOT = NROW * WROW;                     // 16-B slots of one weight step
   constexpr int WBUF = WSLOT * 8;                        // halfs
   constexpr int WPCS = WSLOT / 64;                       // weight pieces per step (24 or 12)
   constexpr int WPW = (WPCS + 7) / 8;                    // per wave (3 or 2; surplus waves duplicate)
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
   const int nslab = C / SLAB;
   const int K = 9 * C;
   const int units_per_tile = nslab;
-  constexpr int SPU = 3;                                 // steps per unit: kernel rows dy = 0, 1, 2
+  constexpr int SPU = 9 / TPS;                           // steps per unit (slab)
   // tiles of this block: t = blockIdx.x + i * gridDim.x
   const int my_tiles = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   const int my_units = my_tiles * units_per_tile;
@@ -107,16 +113,16 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
   };
   // weight pieces of global step gs (kernel row dy of slab) -> ring slot (gs & 1)
   auto dma_w = [&](int gs) {
-    const int u = gs / SPU, dy = gs - u * SPU;
+    const int u = gs / SPU, st = gs - u * SPU;
     const int slab = u % units_per_tile;
 #pragma unroll
     for (int j = 0; j < WPW; ++j) {
       const int piece = (wave * WPW + j) % WPCS;
       const int s = piece * 64 + lane;
       const int n = s / WROW, rem = s - n * WROW;
-      const int dx = rem / CPX, pos = rem - dx * CPX;
+      const int tt = rem / CPX, pos = rem - tt * CPX;
       const int cd = w_pos<CPX>(n, pos);
-      dh_glds16(w1 + (long)n * K + (dy * 3 + dx) * C + slab * SLAB + cd * 8, wbuf + (gs & 1) * WBUF + piece * 512);
+      dh_glds16(w1 + (long)n * K + (st * TPS + tt) * C + slab * SLAB + cd * 8, wbuf + (gs & 1) * WBUF + piece * 512);
     }
   };
 
@@ -128,9 +134,9 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
 
   const int frow = lane & 15, g = lane >> 4;
   const int jh = ng * 16 + g * 4;                        // this lane's 4 output channels (hi rows)
-  f4 acc[2][4];
+  f4 acc[NB][4];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < NB; ++a)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
   const int my_pp = (PP - 1 - wave) / 8 + 1;             // next-slab patch pieces of this wave
@@ -139,27 +145,29 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
   int pend_bt = -1, pend_y0 = 0, pend_x0 = 0;
 
   for (int gs = 0; gs < my_steps; ++gs) {
-    const int u = gs / SPU, dy = gs - u * SPU;
+    const int u = gs / SPU, st = gs - u * SPU;
     // weights of the next step first, then (first step of a unit) the whole next patch slab: the
     // end-of-step wait then leaves exactly the patch pieces in flight, and they land by the end of
     // the unit's second step
     if (gs + 1 < my_steps) dma_w(gs + 1);
-    const bool issue_p = dy == 0 && u + 1 < my_units;
+    const bool issue_p = st == 0 && u + 1 < my_units;
     if (issue_p)
       for (int j = 0; j < my_pp; ++j) dma_patch(u + 1, wave + j * 8);
-    // ---- 3 taps x ND k-depths x (2 x 4) MFMAs
+    // ---- TPS taps x ND k-depths x (NB x 4) MFMAs
     const h16* pb = patch + (u & 1) * PBUF;
     const h16* wb = wbuf + (gs & 1) * WBUF;
 #pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
+    for (int tt = 0; tt < TPS; ++tt) {
+      const int tap = st * TPS + tt;
+      const int dy = tap / 3, dx = tap - dy * 3;
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
         const int cd = d * 4 + g;
-        h8 wf[2], xf[4];
+        h8 wf[NB], xf[4];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int n = (ng + 2 * a) * 16 + frow;
-          wf[a] = *reinterpret_cast<const h8*>(&wb[(n * WROW + dx * CPX + w_pos<CPX>(n, cd)) * 8]);
+        for (int a = 0; a < NB; ++a) {
+          const int n = (DEPTH ? ng + 2 * a : ng * NB + a) * 16 + frow;
+          wf[a] = *reinterpret_cast<const h8*>(&wb[(n * WROW + tt * CPX + w_pos<CPX>(n, cd)) * 8]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -167,13 +175,33 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
           xf[i] = *reinterpret_cast<const h8*>(&pb[(p * CPX + patch_pos<CPX>(p, cd)) * 8]);
         }
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < NB; ++a)
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[a][i] = mfma16(wf[a], xf[i], acc[a][i]);
       }
     }
-    const bool tile_end = dy == SPU - 1 && (u % units_per_tile) == units_per_tile - 1;
-    if (tile_end) {
+    const bool tile_end = st == SPU - 1 && (u % units_per_tile) == units_per_tile - 1;
+    if (!DEPTH && tile_end) {
+      // +bias [ReLU] -> fp16 NHWC; lane: 4 consecutive channels of pixel (row mg*4+i, col frow)
+      int bt, y0, x0;
+      tile_of_unit(u, bt, y0, x0);
+#pragma unroll
+      for (int a = 0; a < NB; ++a) {
+        const int n = (ng * NB + a) * 16 + g * 4;
+        const f4 bv = b1 ? *reinterpret_cast<const f4*>(b1 + n) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int y = y0 + mg * 4 + i, x = x0 + frow;
+          f4 v = acc[a][i] + bv;
+          h4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (h16)(relu_out ? fmaxf(v[r], 0.f) : v[r]);
+          if (y < H && x < W) *reinterpret_cast<h4*>(yout + (((long)bt * H + y) * W + x) * NROW + n) = o;
+          acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+    if (DEPTH && tile_end) {
       // hi + lo + b1 -> ReLU -> * w2 over this lane's 4 channels, then the 4 lane groups
       float bb[4], ww[4];
 #pragma unroll
@@ -182,12 +210,12 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
       for (int i = 0; i < 4; ++i) {
         float part = 0.f;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) part += fmaxf(acc[0][i][r] + acc[1][i][r] + bb[r], 0.f) * ww[r];
+        for (int r = 0; r < 4; ++r) part += fmaxf(acc[0][i][r] + acc[NB - 1][i][r] + bb[r], 0.f) * ww[r];
         part += __shfl_xor(part, 16, 64);
         part += __shfl_xor(part, 32, 64);
         pend[i] = part;
-        acc[0][i] = f4{0.f, 0.f, 0.f, 0.f};
-        acc[1][i] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int a = 0; a < NB; ++a) acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
       }
       if (ng == 1 && lane < 16) {
 #pragma unroll
@@ -202,7 +230,7 @@ __global__ __launch_bounds__(512) void depth_halo_kernel(const h16* __restrict__
       dh_wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
-    if (tile_end) {
+    if (DEPTH && tile_end) {
       if (ng == 0 && lane < 16) {
         const float bias2 = b2[0];
 #pragma unroll
@@ -237,11 +265,35 @@ int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* 
   const int ntiles = (int)nt;
   const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
   if (C == 32)
-    hipLaunchKernelGGL((depth_halo_kernel<32>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1, b1, w2, b2,
-                       depth, H, W, C, tiles_x, tiles_y, ntiles);
+    hipLaunchKernelGGL((halo_conv_kernel<32, 64, 3, true>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1,
+                       b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles);
   else
-    hipLaunchKernelGGL((depth_halo_kernel<64>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1, b1, w2, b2,
-                       depth, H, W, C, tiles_x, tiles_y, ntiles);
+    hipLaunchKernelGGL((halo_conv_kernel<64, 64, 3, true>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1,
+                       b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+// 3x3 / stride 1 / pad 1 conv, Cin % 64 == 0, Cout == 128, epilogue +bias [ReLU] (output_conv1,
+// dpt.py:117, at 296^2): the halo tile cuts the 9x implicit-GEMM input re-read.  Returns 1 when the
+// shape is not one this kernel serves (caller uses the implicit-GEMM conv).
+int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
+                  int Cout, hipStream_t st) {
+  if (Cout != 128 || Cin % 64 != 0) return 1;
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = n > 0 ? n : 256;
+  }
+  const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
+  const long nt = (long)BT * tiles_x * tiles_y;
+  if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
+  const int ntiles = (int)nt;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false>), dim3(grid), dim3(512), 0, st, (const h16*)x, (const h16*)w,
+                     bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu, H, W, Cin,
+                     tiles_x, tiles_y, ntiles);
   VDA_LAUNCH_CHECK();
   return 0;
 }

@@ -29,6 +29,12 @@ extern "C" int vda_debug_timestamps(void* host) {
 #endif
 #include "../../include/vda.h"
 
+// halo-tiled 3x3 kernels (vda_depth.hip)
+int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
+                   int BT, int H, int W, int C, hipStream_t st);
+int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
+                  int Cout, hipStream_t st);
+
 namespace {
 
 constexpr int BK = 64;
@@ -1236,11 +1242,15 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
   if (p.up_h > 0) return launch_reg_conv(p, (hipStream_t)stream);
+  // large 3x3 maps with 128 output channels (output_conv1 at 296^2): halo-tiled kernel (vda_depth.hip)
+  if (g_force_tile < 0 && ks == 3 && stride == 1 && pad == 1 && !pre_relu && !p.epi.res && !p.epi.res2 &&
+      !p.epi.gamma && !p.epi.rowbias && (long)H * W >= 128L * 128L) {
+    rc = vda_conv_halo(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, BT, H, W, Cin, Cout, (hipStream_t)stream);
+    if (rc != 1) return rc;
+  }
   return launch<true>(p, (hipStream_t)stream);
 }
 
-int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
-                   int BT, int H, int W, int C, hipStream_t st);
 
 extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                               float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho,
