@@ -136,9 +136,10 @@ def main():
     roof = None
     if launches.get("enc_fc1"):
         C = model.pretrained.embed_dim
-        M = args.clips_per_gpu * T * ((H // 14) * (W // 14) + 1)
-        flop = 2.0 * M * (4 * C) * C
-        ms = sum(launches["enc_fc1"]) / len(launches["enc_fc1"])
+        rec = launches["enc_fc1"]
+        flop = sum(f for _, f in rec) / len(rec)          # algorithmic 2*M*N*K per launch
+        ms = sum(t for t, _ in rec) / len(rec)
+        M = int(round(flop / (2.0 * 4 * C * C)))
         achieved = flop / (ms * 1e-3) / 1e12
         traffic = None
         pmc = os.path.join(REPO, "profiles", "r01_pmc_fc1.json")

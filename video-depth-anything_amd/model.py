@@ -427,7 +427,7 @@ class VideoDepthAnything(nn.Module):
 
     def _encode(self, P: _Packed, img: torch.Tensor) -> List[torch.Tensor]:
         """DINOv2 get_intermediate_layers (dinov2.py:212-231, :271-321; block.py:104-106):
-        img [BT, 3, H, W] -> 4 tap maps [BT*np, C] fp16 (final LN applied, cls row dropped)."""
+        img [BT, 3, H, W] -> 4 tap maps [BT*np, C] (final LN applied, cls row dropped)."""
         BT, _, H, W = img.shape
         npt = (H // PATCH) * (W // PATCH)
         ntok = npt + 1

@@ -29,12 +29,13 @@ def enable_probe(tags):
 
 
 def take_probe():
-    """Return {tag: [ms per launch]} for the probed launches (synchronises) and disable probing."""
+    """Return {tag: [(ms, flop) per launch]} for the probed launches (synchronises) and disable
+    probing; flop = 2*M*N*K of that launch."""
     global _PROBE
     out = {}
     if _PROBE:
         torch.cuda.synchronize()
-        out = {t: [a.elapsed_time(b) for a, b in ev] for t, ev in _PROBE.items()}
+        out = {t: [(a.elapsed_time(b), fl) for a, b, fl in ev] for t, ev in _PROBE.items()}
     _PROBE = None
     return out
 
@@ -112,7 +113,7 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
     rc = fn(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), M, N, K, e, _stream(x))
     if probe:
         ev1.record()
-        _PROBE[tag].append((ev0, ev1))
+        _PROBE[tag].append((ev0, ev1, 2.0 * M * N * K))
     check(rc, "vda_gemm")
     return out
 
@@ -166,8 +167,9 @@ def conv2d(x: Tensor, w: Tensor, *, ks=3, stride=1, pad=1, bias=None, pre_relu=F
 
 
 def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period: int = 0,
-              rows: Optional[int] = None) -> Tensor:
-    """Row LayerNorm of x [R, C] (row-strided ok).  skip_period=np drops each frame's cls row."""
+              rows: Optional[int] = None, out: Optional[Tensor] = None) -> Tensor:
+    """Row LayerNorm of x [R, C] (row-strided ok).  skip_period=np drops each frame's cls row.
+    ``out`` (contiguous [rows, C]) may be a slice of a larger buffer."""
     dt = _dt(x)
     _need(x, dt, "x")
     _need_contig(gamma, torch.float32, "gamma")
@@ -176,7 +178,10 @@ def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period
     R, C = x.shape
     if rows is None:
         rows = R if skip_period == 0 else (R // (skip_period + 1)) * skip_period
-    out = torch.empty((rows, C), dtype=dt, device=x.device)
+    if out is None:
+        out = torch.empty((rows, C), dtype=dt, device=x.device)
+    _need_contig(out, dt, "out")
+    assert out.shape == (rows, C)
     fn = _lib.lib().vda_layernorm if dt == torch.float16 else _lib.lib().vda_layernorm_f32
     rc = fn(x.data_ptr(), x.stride(0), out.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                                   rows, C, float(eps), int(skip_period), _stream(x))
