@@ -127,11 +127,15 @@ int vda_spatial_attention(const void* qkv, void* out, int32_t B, int32_t N, int3
  * Temporal self-attention across T <= 32 frames at every spatial site.
  * qkv [(B*T)*S, 3*H*D] half (frame-major rows, [q|k|v] columns, heads contiguous);
  * out [(B*T)*S, H*D] half.  D % 8 == 0, D <= 128.
+ * rope_theta > 0 applies the rotary embedding of pe='rope' to q and k first: channel pairs
+ * (2i, 2i+1) of all C = H*D channels of frame t rotate by t * rope_theta^(-2i/C), in fp32 from the
+ * fp16 q/k, rounded back to fp16 (attention.py:403-429, motion_module.py:290-293); 0 = none ('ape',
+ * whose additive table the caller folds into the q/k/v GEMM as a row bias).
  * Replaces motion_module.py:247-335 (rearrange (b f) d c -> (b d) f c, 8-head softmax over f,
  * rearrange back) and attention.py:182-211/:256-293.
  */
 int vda_temporal_attention(const void* qkv, void* out, int32_t B, int32_t T, int32_t S,
-                           int32_t H, int32_t D, float scale, void* stream);
+                           int32_t H, int32_t D, float scale, float rope_theta, void* stream);
 
 /*
  * Bilinear resize, align_corners=True, NHWC half: X [BT, H, W, C] -> Y [BT, Ho, Wo, C].
@@ -200,7 +204,7 @@ int vda_groupnorm_f32(const float* x, float* y, const float* gamma, const float*
 int vda_spatial_attention_f32(const float* qkv, float* out, int32_t B, int32_t N, int32_t H,
                               int32_t D, float scale, void* stream);
 int vda_temporal_attention_f32(const float* qkv, float* out, int32_t B, int32_t T, int32_t S,
-                               int32_t H, int32_t D, float scale, void* stream);
+                               int32_t H, int32_t D, float scale, float rope_theta, void* stream);
 int vda_upsample_bilinear_f32(const float* x, float* y, int32_t BT, int32_t H, int32_t W, int32_t C,
                               int32_t Ho, int32_t Wo, void* stream);
 int vda_patch_im2col_f32(const float* img, float* a, int32_t BT, int32_t H, int32_t W, int32_t Kp,

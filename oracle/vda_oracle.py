@@ -102,6 +102,18 @@ def positional_table(C: int, max_len: int = 32) -> Tensor:
     return pe
 
 
+def rotary(x: Tensor, theta: float = 10000.0) -> Tensor:
+    """attention.py:403-429 apply_rotary_emb for x [N, T, C]: channel pairs (2i, 2i+1) of frame t
+    rotate by t * theta^(-2i/C), in fp32 (restated with real arithmetic)."""
+    N_, T, C = x.shape
+    freqs = 1.0 / (theta ** (torch.arange(0, C, 2)[: C // 2].float() / C))
+    ang = torch.outer(torch.arange(T, dtype=torch.float32), freqs)  # [T, C/2]
+    cs, sn = torch.cos(ang), torch.sin(ang)
+    xr = x.float().reshape(N_, T, C // 2, 2)
+    a, b = xr[..., 0], xr[..., 1]
+    return torch.stack([a * cs - b * sn, a * sn + b * cs], -1).reshape(N_, T, C).to(x.dtype)
+
+
 def temporal_module(sd: Dict[str, Tensor], pre: str, x: Tensor, T: int) -> Tensor:
     """TemporalModule on NCHW frames x [BT, C, h, w] -> same shape.
 
@@ -125,10 +137,14 @@ def temporal_module(sd: Dict[str, Tensor], pre: str, x: Tensor, T: int) -> Tenso
         n = F.layer_norm(y, (C,), sd[f"{tb}norms.{j}.weight"], sd[f"{tb}norms.{j}.bias"], eps=1e-5)
         d = n.shape[1]
         n = n.reshape(B, T, d, C).permute(0, 2, 1, 3).reshape(B * d, T, C)  # (b f) d c -> (b d) f c
-        n = n + sd[ab + "pos_encoder.pe"][:, :T]
+        ape = (ab + "pos_encoder.pe") in sd   # pe='ape' carries the table; 'rope' has none
+        if ape:
+            n = n + sd[ab + "pos_encoder.pe"][:, :T]
         q = F.linear(n, sd[ab + "to_q.weight"])
         k = F.linear(n, sd[ab + "to_k.weight"])
         v = F.linear(n, sd[ab + "to_v.weight"])
+        if not ape:  # motion_module.py:290-293
+            q, k = rotary(q), rotary(k)
 
         def split(t):
             return t.reshape(B * d, T, heads, dh).permute(0, 2, 1, 3)

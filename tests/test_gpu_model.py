@@ -56,3 +56,19 @@ def test_forward_deterministic_and_batch_independent():
     d0, d1 = m(x[:1]), m(x[1:])
     assert torch.equal(d2, m(x))
     assert rel_l1(d2[:1].cpu(), d0.cpu()) < 1e-6 and rel_l1(d2[1:].cpu(), d1.cpu()) < 1e-6
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_rope_variant_matches_reference_golden(fp32):
+    """pe='rope': q/k rotated inside the temporal attention kernels (fp16 and fp32 paths)."""
+    import json
+    from vda_amd.weights import synthetic_state_dict
+    from helpers import GOLDEN
+    with open(os.path.join(GOLDEN, "state_dict_keys_vits_rope.json")) as f:
+        keys = [(k, tuple(s)) for k, s in json.load(f)]
+    m = vda_amd.build_model("vits", synthetic_state_dict(keys), device="cuda", pe="rope")
+    x, depth, _, _ = load_golden("vits_t8_126_rope")
+    d = m(x.cuda(), fp32=fp32).float().cpu()
+    err = rel_l1(d, depth)
+    print(f"rope fp32={fp32}: rel-L1 vs reference = {err:.3e}")
+    assert err <= (1e-5 if fp32 else TOL_FP16)

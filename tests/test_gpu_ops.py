@@ -307,3 +307,22 @@ def test_conv3x3_halo_cout128(Cin, H, W, relu):
     finally:
         lib.vda_debug_force_tile(-1)
     assert rel(y, y2) < 1e-3
+
+
+@pytest.mark.parametrize("T,S,H,D", [(32, 37, 8, 128), (7, 5, 8, 24), (32, 9, 8, 32)])
+def test_temporal_attention_rope(T, S, H, D):
+    """rope_theta > 0: q/k channel pairs rotated by t * theta^(-2i/C) before the softmax (fp16 kernel)."""
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import vda_oracle
+    C = H * D
+    qkv = rnd(T * S, 3 * C, seed=90 + D)
+    y = ops.temporal_attention(h(qkv), 1, T, S, H, D, rope_theta=10000.0)
+    t = qkv.half().float().view(T, S, 3, C).permute(1, 0, 2, 3)  # [S, T, 3, C]
+    q = vda_oracle.rotary(t[:, :, 0].half()).float()  # rotated in fp32, rounded to fp16 like the reference
+    k = vda_oracle.rotary(t[:, :, 1].half()).float()
+    v = t[:, :, 2]
+    sp = lambda z: z.reshape(S, T, H, D).permute(0, 2, 1, 3)  # noqa: E731
+    o = ((sp(q) @ sp(k).transpose(-1, -2)) * D ** -0.5).softmax(-1) @ sp(v)
+    ref = o.permute(2, 0, 1, 3).reshape(T * S, C)
+    assert rel(y, ref) < 3e-3

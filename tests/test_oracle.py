@@ -39,3 +39,22 @@ def test_oracle_taps_match_reference_stats():
         assert abs(float(f.mean()) - mu) <= 1e-4 * max(1.0, abs(mu))
         assert abs(float(f.std()) - sd_) <= 1e-4 * sd_
         assert abs(float(f.abs().mean()) - am) <= 1e-4 * am
+
+
+def test_rope_variant_schema_and_oracle():
+    """pe='rope' (motion_module.py:238-242, 290-293): the module tree has no pos_encoder buffers, like
+    the reference's; the oracle's rotary restatement matches the reference's output."""
+    import vda_amd
+    from vda_amd.weights import synthetic_state_dict
+    with open(os.path.join(GOLDEN, "state_dict_keys_vits_rope.json")) as f:
+        ref = [(k, tuple(s)) for k, s in json.load(f)]
+    m = vda_amd.VideoDepthAnything.from_config("vits", device="meta", pe="rope")
+    mine = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    assert sorted(mine) == sorted(ref)
+    assert not any(k.endswith("pos_encoder.pe") for k, _ in mine)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    x, depth, _, meta = load_golden("vits_t8_126_rope")
+    assert meta["pe"] == "rope"
+    sd = synthetic_state_dict(ref)
+    d = vda_oracle.forward(sd, "vits", x)
+    assert rel_l1(d, depth) <= 1e-5

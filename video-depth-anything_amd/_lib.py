@@ -61,7 +61,7 @@ def _declare(lib):
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
         "vda_groupnorm_workspace": ([I, I, I, I], L),
         "vda_spatial_attention": ([P, P, I, I, I, I, F, P], I),
-        "vda_temporal_attention": ([P, P, I, I, I, I, I, F, P], I),
+        "vda_temporal_attention": ([P, P, I, I, I, I, I, F, F, P], I),
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),
         "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
         "vda_depth_head": ([P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
@@ -72,7 +72,7 @@ def _declare(lib):
         "vda_layernorm_f32": ([P, L, P, P, P, I, I, F, I, P], I),
         "vda_groupnorm_f32": ([P, P, P, P, I, I, I, I, F, P], I),
         "vda_spatial_attention_f32": ([P, P, I, I, I, I, F, P], I),
-        "vda_temporal_attention_f32": ([P, P, I, I, I, I, I, F, P], I),
+        "vda_temporal_attention_f32": ([P, P, I, I, I, I, I, F, F, P], I),
         "vda_upsample_bilinear_f32": ([P, P, I, I, I, I, I, I, P], I),
         "vda_patch_im2col_f32": ([P, P, I, I, I, I, P], I),
         "vda_depth_head_f32": ([P, P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),

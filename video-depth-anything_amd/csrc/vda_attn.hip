@@ -210,9 +210,29 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 //                16s + 8(j>>2) + 4h + (j&3)), A = Vᵀ by ds_read_b64_tr_b16 from a per-wave V tile.
 // DP = head dim padded to a multiple of 16 (zero-filled), NDT = 32-wide output d tiles.
 // =============================================================================================
+// pe='rope' (attention.py:403-429): rotate the 4 channel pairs of an 8-channel q and k fragment of
+// frame t, first channel c0 (even) of C: angle t * theta^(-2i/C) for pair i, fp32 math on the fp16
+// values (the reference's q.float() complex multiply, type_as back to fp16)
+__device__ __forceinline__ void rope_frag(h8& q, h8& k, int t, int c0, int C, float theta) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int i = (c0 >> 1) + j;
+    const float freq = 1.f / powf(theta, (float)(2 * i) / (float)C);
+    float sn, cs;
+    sincosf((float)t * freq, &sn, &cs);
+    const float qa = (float)q[2 * j], qb = (float)q[2 * j + 1];
+    const float ka = (float)k[2 * j], kb = (float)k[2 * j + 1];
+    q[2 * j] = (h16)(qa * cs - qb * sn);
+    q[2 * j + 1] = (h16)(qa * sn + qb * cs);
+    k[2 * j] = (h16)(ka * cs - kb * sn);
+    k[2 * j + 1] = (h16)(ka * sn + kb * cs);
+  }
+}
+
 template <int DP>
 __global__ __launch_bounds__(256) void temporal_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                            int B, int T, int S, int H, int D, float scale_log2) {
+                                                            int B, int T, int S, int H, int D, float scale_log2,
+                                                            float rope_theta) {
   constexpr int NST = DP / 16;
   constexpr int NDT = (DP + 31) / 32;
   constexpr int DP32 = NDT * 32;
@@ -251,6 +271,7 @@ __global__ __launch_bounds__(256) void temporal_attn_kernel(const h16* __restric
     if (active && r32 < T && d0 < D) {
       qf = __builtin_bit_cast(h8, ldg16(qkv + krow + d0));
       kf = __builtin_bit_cast(h8, ldg16(qkv + krow + C + d0));
+      if (rope_theta > 0.f) rope_frag(qf, kf, r32, hh * D + d0, C, rope_theta);
     }
     acc = mfma32(kf, qf, acc);
   }
@@ -323,7 +344,7 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
 }
 
 extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int32_t T, int32_t S,
-                                      int32_t H, int32_t D, float scale, void* stream) {
+                                      int32_t H, int32_t D, float scale, float rope_theta, void* stream) {
   VDA_CHECK_ARG(qkv && out, "null pointer");
   VDA_CHECK_ARG(B > 0 && S > 0 && H > 0, "empty attention");
   VDA_CHECK_ARG(T > 0 && T <= 32, "temporal attention needs 1 <= T <= 32 (PE table length)");
@@ -333,7 +354,7 @@ extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int
   hipStream_t st = (hipStream_t)stream;
   const float sl = scale * 1.4426950408889634f;
   const int dp = (D + 15) / 16 * 16;
-#define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl)
+#define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl, rope_theta)
   switch (dp) {
     case 16: VDA_TA(16); break;
     case 32: VDA_TA(32); break;

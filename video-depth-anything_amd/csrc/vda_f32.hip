@@ -294,7 +294,8 @@ __global__ __launch_bounds__(256) void spatial_attn_f32_kernel(const float* __re
 // ---- temporal attention (fp32) ----------------------------------------------------------------
 // One wave per (b, site, head); lane t < T is query frame t.  qkv rows (b*T + t)*S + s.
 __global__ __launch_bounds__(64) void temporal_attn_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out,
-                                                               int T, int S, int H, int D, float scale) {
+                                                               int T, int S, int H, int D, float scale,
+                                                               float rope_theta) {
   __shared__ float qt[128 * 33];  // Q^T [d][t] (row 33 floats)
   __shared__ float kk[32 * 129];  // K [t][d]
   __shared__ float vv[32 * 129];  // V [t][d]
@@ -304,12 +305,28 @@ __global__ __launch_bounds__(64) void temporal_attn_f32_kernel(const float* __re
   const int b = site / S, s = site - b * S;
   const int C = H * D;
   const long ld = 3L * C;
-  for (int i = lane; i < T * D; i += 64) {
-    const int t = i / D, d = i - t * D;
+  // channel pairs (d, d+1): pe='rope' rotates q and k by t * theta^(-2i/C), i = global pair index
+  // (attention.py:403-429); D is even for every head size (D % 8 == 0 is not required here)
+  const int Dh = D >> 1;
+  for (int i = lane; i < T * Dh; i += 64) {
+    const int t = i / Dh, d = 2 * (i - t * Dh);
     const float* row = qkv + ((long)(b * T + t) * S + s) * ld + h * D + d;
-    qt[d * 33 + t] = row[0];
-    kk[t * 129 + d] = row[C];
+    float qa = row[0], qb = row[1], ka = row[C], kb = row[C + 1];
+    if (rope_theta > 0.f) {
+      const int pi = (h * D + d) >> 1;
+      const float freq = 1.f / powf(rope_theta, (float)(2 * pi) / (float)C);
+      float sn, cs;
+      sincosf((float)t * freq, &sn, &cs);
+      const float q0 = qa * cs - qb * sn, q1 = qa * sn + qb * cs;
+      const float k0 = ka * cs - kb * sn, k1 = ka * sn + kb * cs;
+      qa = q0; qb = q1; ka = k0; kb = k1;
+    }
+    qt[d * 33 + t] = qa;
+    qt[(d + 1) * 33 + t] = qb;
+    kk[t * 129 + d] = ka;
+    kk[t * 129 + d + 1] = kb;
     vv[t * 129 + d] = row[2 * C];
+    vv[t * 129 + d + 1] = row[2 * C + 1];
   }
   __syncthreads();
   if (lane >= T) return;
@@ -541,14 +558,14 @@ extern "C" int vda_spatial_attention_f32(const float* qkv, float* out, int32_t B
 }
 
 extern "C" int vda_temporal_attention_f32(const float* qkv, float* out, int32_t B, int32_t T, int32_t S, int32_t H,
-                                          int32_t D, float scale, void* stream) {
+                                          int32_t D, float scale, float rope_theta, void* stream) {
   VDA_CHECK_ARG(qkv && out, "null pointer");
   VDA_CHECK_ARG(B > 0 && T > 0 && S > 0 && H > 0 && D > 0, "empty attention");
-  VDA_CHECK_ARG(T <= 32 && D <= 128, "temporal attention: T <= 32, D <= 128");
+  VDA_CHECK_ARG(T <= 32 && D <= 128 && D % 2 == 0, "temporal attention: T <= 32, even D <= 128");
   const long blocks = (long)B * S * H;
   VDA_CHECK_ARG(blocks < 0x7fffffffL, "grid too large");
   hipLaunchKernelGGL(temporal_attn_f32_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, qkv, out, T, S,
-                     H, D, scale);
+                     H, D, scale, rope_theta);
   VDA_LAUNCH_CHECK();
   return 0;
 }

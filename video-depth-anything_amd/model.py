@@ -123,14 +123,17 @@ class PositionalEncoding(nn.Module):  # motion_module.py:189-207
 
 
 class TemporalAttention(nn.Module):  # motion_module.py:210-245 over attention.py:30-92
-    def __init__(self, dim, max_len):
+    def __init__(self, dim, max_len, pe="ape"):
         super().__init__()
         self.heads = 8
+        self.pos_embedding_type = pe
         self.to_q = nn.Linear(dim, dim, bias=False)
         self.to_k = nn.Linear(dim, dim, bias=False)
         self.to_v = nn.Linear(dim, dim, bias=False)
         self.to_out = nn.ModuleList([nn.Linear(dim, dim), nn.Dropout(0.0)])
-        self.pos_encoder = PositionalEncoding(dim, max_len)
+        # 'ape': sinusoidal table added before q/k/v (a state_dict buffer); 'rope': rotary q/k over
+        # channel pairs with frequencies computed on the fly (attention.py:403-429; no buffer)
+        self.pos_encoder = PositionalEncoding(dim, max_len) if pe == "ape" else None
 
 
 class GEGLU(nn.Module):  # attention.py:363-384
@@ -146,31 +149,31 @@ class FeedForward(nn.Module):  # attention.py:296-338
 
 
 class TemporalTransformerBlock(nn.Module):  # motion_module.py:136-170
-    def __init__(self, dim, max_len):
+    def __init__(self, dim, max_len, pe="ape"):
         super().__init__()
-        self.attention_blocks = nn.ModuleList([TemporalAttention(dim, max_len) for _ in range(2)])
+        self.attention_blocks = nn.ModuleList([TemporalAttention(dim, max_len, pe) for _ in range(2)])
         self.norms = nn.ModuleList([nn.LayerNorm(dim) for _ in range(2)])
         self.ff = FeedForward(dim)
         self.ff_norm = nn.LayerNorm(dim)
 
 
 class TemporalTransformer3DModel(nn.Module):  # motion_module.py:72-106
-    def __init__(self, C, max_len):
+    def __init__(self, C, max_len, pe="ape"):
         super().__init__()
         self.norm = nn.GroupNorm(32, C, eps=1e-6, affine=True)
         self.proj_in = nn.Linear(C, C)
-        self.transformer_blocks = nn.ModuleList([TemporalTransformerBlock(C, max_len)])
+        self.transformer_blocks = nn.ModuleList([TemporalTransformerBlock(C, max_len, pe)])
         self.proj_out = nn.Linear(C, C)
 
 
 class TemporalModule(nn.Module):  # motion_module.py:32-69 (num_transformer_block=1, dpt_temporal.py:35-40)
-    def __init__(self, C, max_len=32):
+    def __init__(self, C, max_len=32, pe="ape"):
         super().__init__()
-        self.temporal_transformer = TemporalTransformer3DModel(C, max_len)
+        self.temporal_transformer = TemporalTransformer3DModel(C, max_len, pe)
 
 
 class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
-    def __init__(self, in_channels, features, out_channels, num_frames=32):
+    def __init__(self, in_channels, features, out_channels, num_frames=32, pe="ape"):
         super().__init__()
         self.projects = nn.ModuleList([nn.Conv2d(in_channels, oc, 1) for oc in out_channels])
         self.resize_layers = nn.ModuleList([
@@ -193,8 +196,8 @@ class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
                                        nn.Conv2d(32, 1, 1, 1, 0), nn.ReLU(True), nn.Identity())
         self.scratch = s
         self.motion_modules = nn.ModuleList([
-            TemporalModule(out_channels[2], num_frames), TemporalModule(out_channels[3], num_frames),
-            TemporalModule(features, num_frames), TemporalModule(features, num_frames)])
+            TemporalModule(out_channels[2], num_frames, pe), TemporalModule(out_channels[3], num_frames, pe),
+            TemporalModule(features, num_frames, pe), TemporalModule(features, num_frames, pe)])
 
 
 # ---------------------------------------------------------------------------------------------
@@ -224,24 +227,25 @@ class VideoDepthAnything(nn.Module):
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
         super().__init__()
-        if use_bn or use_clstoken or pe != "ape":
-            raise NotImplementedError("only the shipped configuration (use_bn=False, use_clstoken=False, "
-                                      "pe='ape') is on the accelerated path")
+        if use_bn or use_clstoken or pe not in ("ape", "rope"):
+            raise NotImplementedError("only use_bn=False, use_clstoken=False (the shipped configuration) and "
+                                      "pe in ('ape', 'rope') are on the accelerated path")
+        self.pe = pe
         self.intermediate_layer_idx = {k: v["taps"] for k, v in ENCODER_CFG.items()}
         self.encoder = encoder
         self.num_frames = num_frames
         self.features = features
         self.out_channels = list(out_channels)
         self.pretrained = DinoVisionTransformer(encoder)
-        self.head = DPTHeadTemporal(self.pretrained.embed_dim, features, self.out_channels, num_frames)
+        self.head = DPTHeadTemporal(self.pretrained.embed_dim, features, self.out_channels, num_frames, pe)
         self._packed: Dict[str, _Packed] = {}
         self._pos_cache: Dict[tuple, torch.Tensor] = {}
 
     @classmethod
-    def from_config(cls, encoder: str, device="meta"):
+    def from_config(cls, encoder: str, device="meta", pe: str = "ape"):
         """Build without running torch's default initialisers (weights are loaded afterwards)."""
         with torch.device(device):
-            m = cls(**MODEL_CONFIGS[encoder])
+            m = cls(**MODEL_CONFIGS[encoder], pe=pe)
         return m
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -346,8 +350,10 @@ class VideoDepthAnything(nn.Module):
                 wqkv = torch.cat([ab.to_q.weight, ab.to_k.weight, ab.to_v.weight], 0).float()
                 a.qkv_w = _h(wqkv).to(dev)
                 # (n + pe[t]) Wᵀ = n Wᵀ + pe[t] Wᵀ: the PE add (motion_module.py:255-256) becomes a
-                # per-frame fp32 row bias of the fused q/k/v GEMM.
-                a.pe_bias = _f(ab.pos_encoder.pe[0].float() @ wqkv.t()).to(dev)  # [max_len, 3C]
+                # per-frame fp32 row bias of the fused q/k/v GEMM.  'rope' rotates q/k inside the
+                # temporal attention kernel instead (motion_module.py:290-293).
+                a.pe_bias = (_f(ab.pos_encoder.pe[0].float() @ wqkv.t()).to(dev)  # [max_len, 3C]
+                             if ab.pos_encoder is not None else None)
                 a.out_w, a.out_b = _h(ab.to_out[0].weight).to(dev), _f(ab.to_out[0].bias).to(dev)
                 q.attn.append(a)
             q.ffnw, q.ffnb = _f(blk.ff_norm.weight).to(dev), _f(blk.ff_norm.bias).to(dev)
@@ -392,8 +398,12 @@ class VideoDepthAnything(nn.Module):
         h = ops.gemm(xn, q.pin_w, bias=q.pin_b)
         for a in q.attn:
             n = ops.layernorm(h, a.nw, a.nb, 1e-5)
-            qkv = ops.gemm(n, a.qkv_w, rowbias=a.pe_bias, rdiv=S, rmod=T)
-            at = ops.temporal_attention(qkv, B, T, S, 8, C // 8)
+            if a.pe_bias is not None:
+                qkv = ops.gemm(n, a.qkv_w, rowbias=a.pe_bias, rdiv=S, rmod=T)
+                at = ops.temporal_attention(qkv, B, T, S, 8, C // 8)
+            else:  # pe='rope': rotary q/k (theta 1e4, pairs over all C channels) in the attention kernel
+                qkv = ops.gemm(n, a.qkv_w)
+                at = ops.temporal_attention(qkv, B, T, S, 8, C // 8, rope_theta=10000.0)
             h = ops.gemm(at, a.out_w, bias=a.out_b, res=h, out=h)
         n = ops.layernorm(h, q.ffnw, q.ffnb, 1e-5)
         g = ops.gemm(n, q.ff1_w, bias=q.ff1_b, act=ACT_GEGLU)
@@ -608,10 +618,11 @@ def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", 
 VideoDepthAnything.infer_video_depth = _infer_video_depth
 
 
-def build_model(encoder: str = "vitl", state_dict: Optional[dict] = None, device="cuda") -> VideoDepthAnything:
+def build_model(encoder: str = "vitl", state_dict: Optional[dict] = None, device="cuda",
+                pe: str = "ape") -> VideoDepthAnything:
     """Construct, load weights (reference checkpoint dict or the synthetic recipe), move to device."""
     from .weights import synthetic_state_dict
-    m = VideoDepthAnything.from_config(encoder, device="meta")
+    m = VideoDepthAnything.from_config(encoder, device="meta", pe=pe)
     if state_dict is None:
         state_dict = synthetic_state_dict((k, tuple(v.shape)) for k, v in m.state_dict().items())
     m.load_state_dict(state_dict, strict=True, assign=True)

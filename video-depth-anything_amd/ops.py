@@ -220,14 +220,15 @@ def spatial_attention(qkv: Tensor, B: int, N: int, H: int, D: int = 64) -> Tenso
     return out
 
 
-def temporal_attention(qkv: Tensor, B: int, T: int, S: int, H: int, D: int) -> Tensor:
+def temporal_attention(qkv: Tensor, B: int, T: int, S: int, H: int, D: int, rope_theta: float = 0.0) -> Tensor:
+    """Softmax attention over the T frames of every site; ``rope_theta`` > 0 rotates q and k first
+    (pe='rope', attention.py:403-429: pairs (2i, 2i+1) of all H*D channels, angle t * theta^(-2i/C))."""
     dt = _dt(qkv)
     _need_contig(qkv, dt, "qkv")
     assert qkv.shape == (B * T * S, 3 * H * D)
     out = torch.empty((B * T * S, H * D), dtype=dt, device=qkv.device)
     fn = _lib.lib().vda_temporal_attention if dt == torch.float16 else _lib.lib().vda_temporal_attention_f32
-    rc = fn(qkv.data_ptr(), out.data_ptr(), B, T, S, H, D, float(D) ** -0.5,
-                                           _stream(qkv))
+    rc = fn(qkv.data_ptr(), out.data_ptr(), B, T, S, H, D, float(D) ** -0.5, float(rope_theta), _stream(qkv))
     check(rc, "vda_temporal_attention")
     return out
 
