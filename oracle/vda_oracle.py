@@ -54,7 +54,7 @@ def interpolate_pos_encoding(pos_embed: Tensor, H: int, W: int) -> Tensor:
     return torch.cat((cls_pe.unsqueeze(0), patch_pe), dim=1)
 
 
-def encoder_taps(sd: Dict[str, Tensor], enc: str, x: Tensor) -> List[Tensor]:
+def encoder_taps(sd: Dict[str, Tensor], enc: str, x: Tensor, return_cls: bool = False):
     """DINOv2 get_intermediate_layers(x, taps, return_class_token=True) with norm=True.
 
     dinov2.py:212-231 (prepare_tokens), :271-281 (blocks), :297-321 (norm + strip cls);
@@ -88,8 +88,10 @@ def encoder_taps(sd: Dict[str, Tensor], enc: str, x: Tensor) -> List[Tensor]:
         t = t + h * sd[b + "ls2.gamma"]
         if i in cfg["taps"]:
             outs.append(t)
-    outs = [F.layer_norm(o, (C,), sd[p + "norm.weight"], sd[p + "norm.bias"], eps=1e-6)[:, 1:] for o in outs]
-    return outs
+    outs = [F.layer_norm(o, (C,), sd[p + "norm.weight"], sd[p + "norm.bias"], eps=1e-6) for o in outs]
+    if return_cls:  # dinov2.py:311-312: (patch tokens, cls token) per tap
+        return [o[:, 1:] for o in outs], [o[:, 0] for o in outs]
+    return [o[:, 1:] for o in outs]
 
 
 def positional_table(C: int, max_len: int = 32) -> Tensor:
@@ -164,9 +166,15 @@ def temporal_module(sd: Dict[str, Tensor], pre: str, x: Tensor, T: int) -> Tenso
 
 
 def _rcu(sd, pre, x):
-    """blocks.py:68-91 ResidualConvUnit (bn=False, groups=1)."""
-    o = F.conv2d(F.relu(x), sd[pre + "conv1.weight"], sd[pre + "conv1.bias"], padding=1)
-    o = F.conv2d(F.relu(o), sd[pre + "conv2.weight"], sd[pre + "conv2.bias"], padding=1)
+    """blocks.py:68-91 ResidualConvUnit (groups=1; eval BatchNorm after each conv when bn=True)."""
+    def bn(o, j):
+        b = f"{pre}bn{j}."
+        if b + "running_var" not in sd:
+            return o
+        return F.batch_norm(o, sd[b + "running_mean"], sd[b + "running_var"], sd[b + "weight"], sd[b + "bias"],
+                            training=False, eps=1e-5)
+    o = bn(F.conv2d(F.relu(x), sd[pre + "conv1.weight"], sd[pre + "conv1.bias"], padding=1), 1)
+    o = bn(F.conv2d(F.relu(o), sd[pre + "conv2.weight"], sd[pre + "conv2.bias"], padding=1), 2)
     return o + x
 
 
@@ -183,12 +191,17 @@ def _fusion(sd, pre, xs: Sequence[Tensor], size=None):
     return F.conv2d(out, sd[pre + "out_conv.weight"], sd[pre + "out_conv.bias"])
 
 
-def reassemble(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int) -> List[Tensor]:
+def reassemble(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int, cls=None) -> List[Tensor]:
     """DPT reassemble (dpt_temporal.py:55-69 / get_motion_features :101-131, dpt.py:60-90).
-    feats: 4 x [BT, ph*pw, C] -> layer_1..4 NCHW."""
+    feats: 4 x [BT, ph*pw, C] -> layer_1..4 NCHW.  With readout projections (use_clstoken,
+    dpt.py:92-98, :129-132) each token is GELU(Linear([token, cls]))."""
     hp = "head."
     out = []
     for i, t in enumerate(feats):
+        if (f"{hp}readout_projects.{i}.0.weight") in sd:
+            rd = cls[i].unsqueeze(1).expand_as(t)
+            t = F.gelu(F.linear(torch.cat((t, rd), -1), sd[f"{hp}readout_projects.{i}.0.weight"],
+                                sd[f"{hp}readout_projects.{i}.0.bias"]))
         x = t.permute(0, 2, 1).reshape(t.shape[0], t.shape[-1], ph, pw)
         x = F.conv2d(x, sd[f"{hp}projects.{i}.weight"], sd[f"{hp}projects.{i}.bias"])
         if i == 0:
@@ -231,9 +244,9 @@ def head_from_layers(sd: Dict[str, Tensor], l1: Tensor, l2: Tensor, l3: Tensor, 
 
 
 def dpt_temporal_head(sd: Dict[str, Tensor], feats: List[Tensor], ph: int, pw: int, T: int,
-                      skip_tmp_block: bool = False) -> Tensor:
+                      skip_tmp_block: bool = False, cls=None) -> Tensor:
     """dpt_temporal.py:53-99 (+ dpt.py:47-124, blocks.py).  feats: 4 x [BT, ph*pw, C]."""
-    l1, l2, l3, l4 = reassemble(sd, feats, ph, pw)
+    l1, l2, l3, l4 = reassemble(sd, feats, ph, pw, cls)
     return head_from_layers(sd, l1, l2, l3, l4, ph, pw, T, skip_tmp_block)
 
 
@@ -250,7 +263,8 @@ class StreamEngine:
     def motion_features(self, x: Tensor):
         x = x.float().cpu()
         ph, pw = x.shape[-2] // PATCH, x.shape[-1] // PATCH
-        return tuple(reassemble(self.sd, encoder_taps(self.sd, self.enc, x), ph, pw))
+        feats, cls = encoder_taps(self.sd, self.enc, x, return_cls=True)
+        return tuple(reassemble(self.sd, feats, ph, pw, cls))
 
     @torch.no_grad()
     def predict(self, x: Tensor, old, pred_idx, T: int, skip_tmp_block: bool = False):
@@ -278,8 +292,8 @@ def forward(sd: Dict[str, Tensor], enc: str, x: Tensor, skip_tmp_block: bool = F
     x = x.float().cpu()
     B, T, _, H, W = x.shape
     ph, pw = H // PATCH, W // PATCH
-    feats = encoder_taps(sd, enc, x.flatten(0, 1))
-    d = dpt_temporal_head(sd, feats, ph, pw, T, skip_tmp_block)
+    feats, cls = encoder_taps(sd, enc, x.flatten(0, 1), return_cls=True)
+    d = dpt_temporal_head(sd, feats, ph, pw, T, skip_tmp_block, cls)
     d = F.interpolate(d, size=(H, W), mode="bilinear", align_corners=True)
     return F.relu(d).squeeze(1).unflatten(0, (B, T))
 

@@ -64,7 +64,7 @@ def test_conv_and_attention_validation():
     e = _lib.Epilogue()
     assert lib.vda_conv2d(fake, fake, fake, 1, 8, 8, 12, 16, 3, 1, 1, 0, 0, 0, e, None) == -22  # Cin % 8
     assert lib.vda_spatial_attention(fake, fake, 1, 10, 2, 32, 0.1, None) == -22                # D != 64
-    assert lib.vda_temporal_attention(fake, fake, 1, 33, 4, 8, 16, 0.1, None) == -22          # T > 32
+    assert lib.vda_temporal_attention(fake, fake, 1, 33, 4, 8, 16, 0.1, 0.0, None) == -22     # T > 32
     assert b"T <= 32" in lib.vda_last_error()
     assert lib.vda_patch_im2col(fake, fake, 1, 20, 28, 592, None) == -22                      # H % 14
     assert b"multiples of the patch size" in lib.vda_last_error()

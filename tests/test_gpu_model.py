@@ -72,3 +72,20 @@ def test_rope_variant_matches_reference_golden(fp32):
     err = rel_l1(d, depth)
     print(f"rope fp32={fp32}: rel-L1 vs reference = {err:.3e}")
     assert err <= (1e-5 if fp32 else TOL_FP16)
+
+
+@pytest.mark.parametrize("fp32", [False, True])
+def test_bn_clstoken_variant_matches_reference_golden(fp32):
+    """use_bn=True (BatchNorm folded into the RCU convs) + use_clstoken=True (readout as a per-frame
+    fp32 row bias + GELU epilogue of the patch GEMM) vs the reference's output."""
+    import json
+    from vda_amd.weights import synthetic_state_dict
+    from helpers import GOLDEN
+    with open(os.path.join(GOLDEN, "state_dict_keys_vits_bn_cls.json")) as f:
+        keys = [(k, tuple(s)) for k, s in json.load(f)]
+    m = vda_amd.build_model("vits", synthetic_state_dict(keys), device="cuda", use_bn=True, use_clstoken=True)
+    x, depth, _, _ = load_golden("vits_t4_70x98_bn_cls")
+    d = m(x.cuda(), fp32=fp32).float().cpu()
+    err = rel_l1(d, depth)
+    print(f"bn+clstoken fp32={fp32}: rel-L1 vs reference = {err:.3e}")
+    assert err <= (1e-5 if fp32 else TOL_FP16)

@@ -58,3 +58,20 @@ def test_rope_variant_schema_and_oracle():
     sd = synthetic_state_dict(ref)
     d = vda_oracle.forward(sd, "vits", x)
     assert rel_l1(d, depth) <= 1e-5
+
+
+def test_bn_clstoken_variant_schema_and_oracle():
+    """use_bn=True, use_clstoken=True: the same key schema as the reference's tree (BatchNorm buffers,
+    readout projections) and the oracle reproduces the reference's output."""
+    import vda_amd
+    from vda_amd.weights import synthetic_state_dict
+    with open(os.path.join(GOLDEN, "state_dict_keys_vits_bn_cls.json")) as f:
+        ref = [(k, tuple(s)) for k, s in json.load(f)]
+    with torch.device("meta"):
+        m = vda_amd.VideoDepthAnything(**vda_amd.MODEL_CONFIGS["vits"], use_bn=True, use_clstoken=True)
+    mine = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    assert sorted(mine) == sorted(ref)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    x, depth, _, meta = load_golden("vits_t4_70x98_bn_cls")
+    d = vda_oracle.forward(synthetic_state_dict(ref), "vits", x)
+    assert rel_l1(d, depth) <= 1e-5

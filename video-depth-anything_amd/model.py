@@ -97,18 +97,22 @@ class DinoVisionTransformer(nn.Module):  # dinov2.py:44-170, DINOv2() factory :3
 
 
 class ResidualConvUnit(nn.Module):  # blocks.py:37-66
-    def __init__(self, f):
+    def __init__(self, f, bn=False):
         super().__init__()
+        self.bn = bn
         self.conv1 = nn.Conv2d(f, f, 3, 1, 1, bias=True)
         self.conv2 = nn.Conv2d(f, f, 3, 1, 1, bias=True)
+        if bn:  # blocks.py:60-62 (eval mode: folded into the convs when packing)
+            self.bn1 = nn.BatchNorm2d(f)
+            self.bn2 = nn.BatchNorm2d(f)
 
 
 class FeatureFusionBlock(nn.Module):  # blocks.py:94-133
-    def __init__(self, f):
+    def __init__(self, f, bn=False):
         super().__init__()
         self.out_conv = nn.Conv2d(f, f, 1, 1, 0, bias=True)
-        self.resConfUnit1 = ResidualConvUnit(f)
-        self.resConfUnit2 = ResidualConvUnit(f)
+        self.resConfUnit1 = ResidualConvUnit(f, bn)
+        self.resConfUnit2 = ResidualConvUnit(f, bn)
 
 
 class PositionalEncoding(nn.Module):  # motion_module.py:189-207
@@ -173,9 +177,14 @@ class TemporalModule(nn.Module):  # motion_module.py:32-69 (num_transformer_bloc
 
 
 class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
-    def __init__(self, in_channels, features, out_channels, num_frames=32, pe="ape"):
+    def __init__(self, in_channels, features, out_channels, num_frames=32, pe="ape", use_bn=False,
+                 use_clstoken=False):
         super().__init__()
+        self.use_clstoken = use_clstoken
         self.projects = nn.ModuleList([nn.Conv2d(in_channels, oc, 1) for oc in out_channels])
+        if use_clstoken:  # dpt.py:92-98: Linear(2C -> C) + GELU on [patch token, cls token]
+            self.readout_projects = nn.ModuleList([
+                nn.Sequential(nn.Linear(2 * in_channels, in_channels), nn.GELU()) for _ in out_channels])
         self.resize_layers = nn.ModuleList([
             nn.ConvTranspose2d(out_channels[0], out_channels[0], 4, 4, 0),
             nn.ConvTranspose2d(out_channels[1], out_channels[1], 2, 2, 0),
@@ -187,10 +196,10 @@ class DPTHeadTemporal(nn.Module):  # dpt.py:47-124 + dpt_temporal.py:23-51
         s.layer2_rn = nn.Conv2d(out_channels[1], features, 3, 1, 1, bias=False)
         s.layer3_rn = nn.Conv2d(out_channels[2], features, 3, 1, 1, bias=False)
         s.layer4_rn = nn.Conv2d(out_channels[3], features, 3, 1, 1, bias=False)
-        s.refinenet1 = FeatureFusionBlock(features)
-        s.refinenet2 = FeatureFusionBlock(features)
-        s.refinenet3 = FeatureFusionBlock(features)
-        s.refinenet4 = FeatureFusionBlock(features)
+        s.refinenet1 = FeatureFusionBlock(features, use_bn)
+        s.refinenet2 = FeatureFusionBlock(features, use_bn)
+        s.refinenet3 = FeatureFusionBlock(features, use_bn)
+        s.refinenet4 = FeatureFusionBlock(features, use_bn)
         s.output_conv1 = nn.Conv2d(features, features // 2, 3, 1, 1)
         s.output_conv2 = nn.Sequential(nn.Conv2d(features // 2, 32, 3, 1, 1), nn.ReLU(True),
                                        nn.Conv2d(32, 1, 1, 1, 0), nn.ReLU(True), nn.Identity())
@@ -227,25 +236,27 @@ class VideoDepthAnything(nn.Module):
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
         super().__init__()
-        if use_bn or use_clstoken or pe not in ("ape", "rope"):
-            raise NotImplementedError("only use_bn=False, use_clstoken=False (the shipped configuration) and "
-                                      "pe in ('ape', 'rope') are on the accelerated path")
+        if pe not in ("ape", "rope"):
+            raise NotImplementedError(pe)  # motion_module.py:243-244
         self.pe = pe
+        self.use_bn, self.use_clstoken = bool(use_bn), bool(use_clstoken)
         self.intermediate_layer_idx = {k: v["taps"] for k, v in ENCODER_CFG.items()}
         self.encoder = encoder
         self.num_frames = num_frames
         self.features = features
         self.out_channels = list(out_channels)
         self.pretrained = DinoVisionTransformer(encoder)
-        self.head = DPTHeadTemporal(self.pretrained.embed_dim, features, self.out_channels, num_frames, pe)
+        self.head = DPTHeadTemporal(self.pretrained.embed_dim, features, self.out_channels, num_frames, pe,
+                                    self.use_bn, self.use_clstoken)
         self._packed: Dict[str, _Packed] = {}
         self._pos_cache: Dict[tuple, torch.Tensor] = {}
 
     @classmethod
-    def from_config(cls, encoder: str, device="meta", pe: str = "ape"):
+    def from_config(cls, encoder: str, device="meta", pe: str = "ape", use_bn: bool = False,
+                    use_clstoken: bool = False):
         """Build without running torch's default initialisers (weights are loaded afterwards)."""
         with torch.device(device):
-            m = cls(**MODEL_CONFIGS[encoder], pe=pe)
+            m = cls(**MODEL_CONFIGS[encoder], pe=pe, use_bn=use_bn, use_clstoken=use_clstoken)
         return m
 
     def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
@@ -296,6 +307,13 @@ class VideoDepthAnything(nn.Module):
         P.nw, P.nb = _f(enc.norm.weight).to(dev), _f(enc.norm.bias).to(dev)
 
         hd = self.head
+        if self.use_clstoken:  # readout Linear(2C -> C): [patch | cls] halves (dpt.py:92-98, :129-132)
+            P.ro_wa, P.ro_wb, P.ro_b = [], [], []
+            for rp in hd.readout_projects:
+                w = rp[0].weight.detach().float()
+                P.ro_wa.append(_h(w[:, :C]).to(dev))
+                P.ro_wb.append(w[:, C:].contiguous().to(dev))  # fp32: the per-frame cls term, exact
+                P.ro_b.append(_f(rp[0].bias).to(dev))
         P.proj_w = [_h(c.weight.reshape(c.weight.shape[0], -1)).to(dev) for c in hd.projects]
         P.proj_b = [_f(c.bias).to(dev) for c in hd.projects]
         P.rs_w, P.rs_b = {}, {}
@@ -315,10 +333,16 @@ class VideoDepthAnything(nn.Module):
             q.out_w, q.out_b = _h(r.out_conv.weight.reshape(r.out_conv.weight.shape[0], -1)).to(dev), _f(r.out_conv.bias).to(dev)
             for u in (1, 2):
                 rcu = getattr(r, f"resConfUnit{u}")
-                setattr(q, f"r{u}c1_w", _conv_nhwc(rcu.conv1.weight).to(dev))
-                setattr(q, f"r{u}c1_b", _f(rcu.conv1.bias).to(dev))
-                setattr(q, f"r{u}c2_w", _conv_nhwc(rcu.conv2.weight).to(dev))
-                setattr(q, f"r{u}c2_b", _f(rcu.conv2.bias).to(dev))
+                for c in (1, 2):
+                    conv = getattr(rcu, f"conv{c}")
+                    w, b = conv.weight.detach().float(), conv.bias.detach().float()
+                    if rcu.bn:  # eval BatchNorm after the conv (blocks.py:79-85), folded exactly in fp32
+                        bnm = getattr(rcu, f"bn{c}")
+                        sc = bnm.weight.detach().float() / torch.sqrt(bnm.running_var.detach().float() + bnm.eps)
+                        w = w * sc[:, None, None, None]
+                        b = (b - bnm.running_mean.detach().float()) * sc + bnm.bias.detach().float()
+                    setattr(q, f"r{u}c{c}_w", _conv_nhwc(w).to(dev))
+                    setattr(q, f"r{u}c{c}_b", _f(b).to(dev))
             P.ref[i] = q
         P.oc1_w, P.oc1_b = _conv_nhwc(s.output_conv1.weight).to(dev), _f(s.output_conv1.bias).to(dev)
         oc2 = s.output_conv2
@@ -435,9 +459,10 @@ class VideoDepthAnything(nn.Module):
         if T > self.num_frames:  # PE table length (motion_module.py:198-206)
             raise ValueError(f"clip length {T} exceeds the temporal PE table ({self.num_frames})")
 
-    def _encode(self, P: _Packed, img: torch.Tensor) -> List[torch.Tensor]:
+    def _encode(self, P: _Packed, img: torch.Tensor):
         """DINOv2 get_intermediate_layers (dinov2.py:212-231, :271-321; block.py:104-106):
-        img [BT, 3, H, W] -> 4 tap maps [BT*np, C] (final LN applied, cls row dropped)."""
+        img [BT, 3, H, W] -> (4 tap maps [BT*np, C] (final LN applied, cls row dropped),
+        4 normed cls rows [BT, C] when use_clstoken else None)."""
         BT, _, H, W = img.shape
         npt = (H // PATCH) * (W // PATCH)
         ntok = npt + 1
@@ -446,6 +471,7 @@ class VideoDepthAnything(nn.Module):
         del a
         taps = self.intermediate_layer_idx[self.encoder]
         feats: List[torch.Tensor] = []
+        cls: Optional[List[torch.Tensor]] = [] if self.use_clstoken else None
         for i, q in enumerate(P.blocks):
             hN = ops.layernorm(tok, q.n1w, q.n1b, 1e-6)
             qkv = ops.gemm(hN, q.qkv_w, bias=q.qkv_b)
@@ -458,14 +484,22 @@ class VideoDepthAnything(nn.Module):
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
                 feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
-        return feats
+                if cls is not None:  # the same norm on each frame's cls row (row stride ntok*C)
+                    cls.append(ops.layernorm(tok.view(BT, ntok, -1)[:, 0], P.nw, P.nb, 1e-6))
+        return feats, cls
 
-    def _reassemble(self, P: _Packed, feats: List[torch.Tensor], BT: int, ph: int, pw: int) -> List[torch.Tensor]:
+    def _reassemble(self, P: _Packed, enc, BT: int, ph: int, pw: int) -> List[torch.Tensor]:
         """DPT reassemble (dpt_temporal.py:55-69 == get_motion_features :101-131, dpt.py:60-90):
-        -> layer_1..4 NHWC fp16 [BT, h, w, C]."""
+        enc = _encode's (taps, cls) -> layer_1..4 NHWC [BT, h, w, C]."""
+        feats, cls = enc
         oc = self.out_channels
         lay = []
         for i, ft in enumerate(feats):
+            if cls is not None:
+                # readout (dpt.py:129-132): GELU(W [x | cls] + b) = GELU(W_a x + (W_b cls + b)): the cls
+                # term is one fp32 row per frame, a row bias of the patch GEMM
+                rb = ops.gemm(cls[i].float(), P.ro_wb[i], bias=P.ro_b[i])
+                ft = ops.gemm(ft, P.ro_wa[i], rowbias=rb, rdiv=ph * pw, rmod=BT, act=ACT_GELU)
             p = ops.gemm(ft, P.proj_w[i], bias=P.proj_b[i])
             if i == 0:
                 l = ops.conv_transpose_ks(p, P.rs_w[0], P.rs_b[0], BT, ph, pw, 4)
@@ -619,10 +653,10 @@ VideoDepthAnything.infer_video_depth = _infer_video_depth
 
 
 def build_model(encoder: str = "vitl", state_dict: Optional[dict] = None, device="cuda",
-                pe: str = "ape") -> VideoDepthAnything:
+                pe: str = "ape", use_bn: bool = False, use_clstoken: bool = False) -> VideoDepthAnything:
     """Construct, load weights (reference checkpoint dict or the synthetic recipe), move to device."""
     from .weights import synthetic_state_dict
-    m = VideoDepthAnything.from_config(encoder, device="meta", pe=pe)
+    m = VideoDepthAnything.from_config(encoder, device="meta", pe=pe, use_bn=use_bn, use_clstoken=use_clstoken)
     if state_dict is None:
         state_dict = synthetic_state_dict((k, tuple(v.shape)) for k, v in m.state_dict().items())
     m.load_state_dict(state_dict, strict=True, assign=True)

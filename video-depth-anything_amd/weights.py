@@ -15,6 +15,7 @@ Recipe, per key (generator seeded with crc32(key)):
   * conv / linear weights          N(0,1) / sqrt(fan_in)
   * ``head.scratch.output_conv2.2`` weight |N(0,1)|/sqrt(32), bias 0.05: keeps the depth strictly
     positive so the final ReLUs (dpt.py:122, video_depth.py:64) do not zero most of the map.
+  * BatchNorm (use_bn=True): running_mean 0.1 N(0,1), running_var U(0.5, 1.5), num_batches_tracked 0.
 """
 from __future__ import annotations
 
@@ -46,6 +47,12 @@ def synthetic_tensor(key: str, shape: Tuple[int, ...]) -> torch.Tensor:
     if key == "head.scratch.output_conv2.2.bias":
         return torch.full(shape, 0.05)
     leaf = key.rsplit(".", 1)[-1]
+    if leaf == "num_batches_tracked":  # BatchNorm bookkeeping (use_bn=True trees)
+        return torch.zeros(shape, dtype=torch.long)
+    if leaf == "running_var":
+        return 0.5 + torch.rand(shape, generator=g)
+    if leaf == "running_mean":
+        return 0.1 * torch.randn(shape, generator=g)
     if leaf == "gamma":
         return 0.2 + 0.4 * torch.rand(shape, generator=g)
     if leaf == "weight" and len(shape) == 1:  # norm affine
