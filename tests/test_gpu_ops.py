@@ -326,3 +326,40 @@ def test_temporal_attention_rope(T, S, H, D):
     o = ((sp(q) @ sp(k).transpose(-1, -2)) * D ** -0.5).softmax(-1) @ sp(v)
     ref = o.permute(2, 0, 1, 3).reshape(T * S, C)
     assert rel(y, ref) < 3e-3
+
+
+@pytest.mark.parametrize("Cin,H,W,BT,mode", [(256, 148, 148, 2, "rcu2"), (256, 74, 74, 3, "rcu1"), (1024, 37, 37, 2, "plain"),
+                                             (64, 17, 160, 2, "rcu2"), (32, 9, 16, 3, "rcu1"), (512, 5, 23, 2, "plain")])
+def test_conv3x3_strip_cout256(Cin, H, W, BT, mode):
+    """3x3 convs with 256 outputs on maps <= 160 wide on the strip-tiled halo kernel (layerN_rn,
+    blocks.py:20-32; RCU conv1 with pre-ReLU + ReLU, conv2 with the skip and fusion adds,
+    blocks.py:78-91 / :146-150); partial last tiles, tiles spanning 3 rows, Cin = 32 .. 1024.
+    vs torch fp32 and vs the implicit-GEMM conv (vda_debug_force_tile(-2))."""
+    x = rnd(BT, Cin, H, W, seed=90)
+    w, b = rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=91), rnd(256, scale=0.1, seed=92)
+    r1, r2 = rnd(BT, 256, H, W, seed=93), rnd(BT, 256, H, W, seed=94)
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    kw = {}
+    if mode == "plain":
+        ref = F.conv2d(x, w, padding=1)
+    elif mode == "rcu1":
+        ref = F.relu(F.conv2d(F.relu(x), w, b, padding=1))
+        kw = dict(bias=f32(b), pre_relu=True, act=ACT_RELU)
+    else:
+        ref = F.conv2d(x, w, b, padding=1) + r1 + r2
+        kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
+    ref = ref.permute(0, 2, 3, 1)
+    xh, wh = nh(x), nh(w)
+    lib = vda_amd._libvda()
+    lib.vda_debug_force_tile(-3)  # strip kernel for every Cin (the default takes it for Cin >= 512)
+    try:
+        y = ops.conv2d(xh, wh, **kw)
+    finally:
+        lib.vda_debug_force_tile(-1)
+    assert rel(y, ref) < 2e-3
+    lib.vda_debug_force_tile(-2)
+    try:
+        y2 = ops.conv2d(xh, wh, **kw)
+    finally:
+        lib.vda_debug_force_tile(-1)
+    assert rel(y, y2) < 1e-3

@@ -2,6 +2,7 @@
 #include "vda_common.h"
 #include "../../include/vda.h"
 #include <type_traits>
+#include <stdlib.h>
 
 namespace {
 
@@ -204,6 +205,185 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 }
 
 // =============================================================================================
+// Spatial attention v2, D = 64, v_mfma_f32_32x32x16_f16 (the 32-cycle MFMA leaves 24 issue cycles
+// per gap for the softmax VALU, the 16x16x32 one only 8).  Block = 4 waves x 32 queries of one
+// (batch, head); a wave owns 32 query columns, a lane q = lane & 31 and half hf = lane >> 5.
+//   Sᵀ[key][q] = K·Qᵀ   A = K rows (LDS, ds_read_b128), B = Q (registers, pre-scaled by scale·log2e);
+//                       the chain starts from C = -m (a 16-register tile of the running max), so
+//                       the scores come out relative to the max with no VALU subtraction.
+//   Oᵀ += Vᵀ·Pᵀ         B = P straight from the Sᵀ registers (k order 16st + 8(j>>2) + 4hf + (j&3)),
+//                       A = Vᵀ by ds_read_b64_tr_b16 in the same permuted key order.
+// K/V tiles (64 keys x 64 channels, 8 KiB each) arrive by LDS-DMA into a 3-deep ring (4 x 1-KiB
+// pieces per wave per tile, keys >= N from a zero page), one barrier per tile.  The block -> (b, h,
+// query block) map keeps all query blocks of one (b, h) on one XCD (K/V re-reads hit that L2).
+// LDS images: K slot row*8 + (chunk ^ ((row >> 1) & 7)), V slot row*8 + (chunk ^ (((row >> 1) & 1) << 2)):
+// conflict-free for the b128 K reads and the b64 transposed V reads (brute-forced).
+// =============================================================================================
+constexpr int SA_KT = 64;    // keys per tile
+constexpr int SA_QB = 128;   // queries per block
+constexpr int SA_NBUF = 3;   // K/V ring depth
+
+__device__ __forceinline__ int sa_kslot(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
+__device__ __forceinline__ int sa_vslot(int row, int c) { return row * 8 + (c ^ (((row >> 1) & 1) << 2)); }
+__global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                                int N, int H, int nqb, int nblocks, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) h16 sKV[SA_NBUF][2][SA_KT * SD];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int id = blockIdx.x;
+  const int per = nblocks >> 3;
+  if (id < per * 8) id = (id & 7) * per + (id >> 3);
+  const int qb = __builtin_amdgcn_readfirstlane(id % nqb), bh = id / nqb;  // scalar (the buffer
+  const int h = __builtin_amdgcn_readfirstlane(bh % H), b = __builtin_amdgcn_readfirstlane(bh / H);  // rsrc)
+  const int C = H * SD;
+  const long ld = 3L * C;
+  const h16* base = qkv + (long)b * N * ld + h * SD;
+  const int r32 = lane & 31, hf = lane >> 5;
+  const int q = qb * SA_QB + wave * 32 + r32;
+
+  h8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    h8 t = h8{0, 0, 0, 0, 0, 0, 0, 0};
+    if (q < N) t = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + ks * 16 + hf * 8));
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (h16)((float)t[e] * scale_log2);
+    qf[ks] = t;
+  }
+
+  // 16 pieces per tile (8 K + 8 V, 8 key rows each); wave w moves pieces 4w .. 4w+3.  Buffer loads
+  // with the (b, h) rows as the record range: keys >= N read as zeros.  Per-lane offsets are fixed
+  // across tiles (the tile advances by the scalar offset).
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
+  unsigned voff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
+    const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
+    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
+    voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
+  }
+  auto dma = [&](int kt) {
+    const int buf = kt % SA_NBUF;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
+                                               (int)(kt * SA_KT * ld * 2), 0, 0);
+    }
+  };
+
+  f16x o[2] = {f16x{}, f16x{}};
+  f16x negm = {};
+  float mrun = 0.f, lsum = 0.f;
+  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+
+  auto tile = [&](int kt, auto first_tag, auto mask_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr bool MASK = decltype(mask_tag)::value;
+    const h16* sk = sKV[kt % SA_NBUF][0];
+    const h16* sv = sKV[kt % SA_NBUF][1];
+    f16x s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const h8 kf = *reinterpret_cast<const h8*>(&sk[sa_kslot(kb * 32 + r32, ks * 2 + hf) * 8]);
+        s[kb] = mfma32(kf, qf[ks], ks == 0 ? negm : s[kb]);
+      }
+    }
+    if constexpr (MASK) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) s[kb][r] = -INFINITY;
+    }
+    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
+    mx = fmaxf(fmaxf(mx, s[0][15]), s[1][0]);
+#pragma unroll
+    for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
+    mx = fmaxf(mx, s[1][15]);
+    mx = half_max(mx);
+    // deferred rescale: keep a stale max while the tile max exceeds it by <= 8 (P <= 2^8: exact in
+    // fp16 P and fp32 sums); the first tile always re-bases
+    if (FIRST || __any(mx > 8.f)) {
+      const float sh = FIRST ? mx : fmaxf(mx, 0.f);
+      mrun += sh;
+      if (!FIRST) {
+        const float alpha = __builtin_amdgcn_exp2f(-sh);
+        lsum *= alpha;
+        o[0] *= alpha;
+        o[1] *= alpha;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -mrun;
+      s[0] -= sh;
+      s[1] -= sh;
+    }
+    h8 pf[4];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(s[kb][r]);
+        lsum += p;
+        pf[kb * 2 + (r >> 3)][r & 7] = (h16)p;
+      }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const int col = dt * 32 + (grp & 1) * 16 + 4 * p4;
+        const int r0 = ps * 16 + 4 * (grp >> 1) + q4;
+        const h4 v0 = lds_read_tr16(&sv[sa_vslot(r0, col >> 3) * 8 + (col & 7)]);
+        const h4 v1 = lds_read_tr16(&sv[sa_vslot(r0 + 8, col >> 3) * 8 + (col & 7)]);
+        const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        o[dt] = mfma32(vf, pf[ps], o[dt]);
+      }
+    }
+  };
+  const int ntiles = (N + SA_KT - 1) / SA_KT;
+  auto enter = [&](int kt) {  // tile kt landed and visible; ring slot of kt-1 free -> prefetch kt+2
+    if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < ntiles) dma(kt + 2);
+  };
+  dma(0);
+  if (ntiles > 1) dma(1);
+  const bool tail = N % SA_KT != 0;
+  enter(0);
+  if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{});
+  else tile(0, std::true_type{}, std::false_type{});
+  const int nfull = ntiles - (tail ? 1 : 0);
+  for (int kt = 1; kt < nfull; ++kt) {
+    enter(kt);
+    tile(kt, std::false_type{}, std::false_type{});
+  }
+  if (tail && ntiles > 1) {
+    enter(ntiles - 1);
+    tile(ntiles - 1, std::false_type{}, std::true_type{});
+  }
+  // epilogue: lane holds Oᵀ[d = dt*32 + 8gq + 4hf + r][q]
+  const float inv = 1.f / half_sum(lsum);
+  if (q < N) {
+    h16* op = out + ((long)b * N + q) * C + h * SD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        h4 v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (h16)(o[dt][gq * 4 + r] * inv);
+        *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
+      }
+  }
+}
+
+// =============================================================================================
 // Temporal attention: one wave per (batch, site s, head), T <= 32 frames, v_mfma_f32_32x32x16_f16.
 //   Sᵀ[key][q] = Σ_d K[key][d] Q[q][d]       A = K rows, B = Q rows (fragments straight from HBM)
 //   Oᵀ[d][q]   = Σ_key Vᵀ[d][key] Pᵀ[key][q]  B = Pᵀ accumulator registers 8s..8s+7 (k order
@@ -336,9 +516,18 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
   VDA_CHECK_ARG(qkv && out, "null pointer");
   VDA_CHECK_ARG(B > 0 && N > 0 && H > 0, "empty attention");
   VDA_CHECK_ARG(D == SD, "spatial attention supports head dim 64 only");
-  dim3 grid((N + SQB - 1) / SQB, H, B);
-  hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
-                     (h16*)out, N, H, scale * 1.4426950408889634f);
+  static const bool old_kernel = getenv("VDA_ATTN_OLD") != nullptr;  // A/B only
+  if (old_kernel) {
+    dim3 grid((N + SQB - 1) / SQB, H, B);
+    hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
+                       (h16*)out, N, H, scale * 1.4426950408889634f);
+  } else {
+    const int nqb = (N + SA_QB - 1) / SA_QB;
+    const long nb = (long)nqb * H * B;
+    VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
+    hipLaunchKernelGGL(spatial_attn32_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
+                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
+  }
   VDA_LAUNCH_CHECK();
   return 0;
 }

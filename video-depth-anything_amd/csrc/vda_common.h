@@ -69,12 +69,26 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Exchange with the partner lane across 16-lane rows (lane ^ 16) resp. wave halves (lane ^ 32):
+// v_permlane16/32_swap with both operands holding v leaves {own, partner} in the pair.  Inline asm
+// because the ROCm 7.2 builtins miscompile exactly this case: with the same value for both operands
+// the second result is read from the first's register (the fmax / add of the pair folds to one
+// value).  s_nop 1 = the 2 wait states a VALU write needs before the swap reads it.
+__device__ __forceinline__ void swap16_pair(float v, float& a, float& b) {
+  a = v; b = v;
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ void swap32_pair(float v, float& a, float& b) {
+  a = v; b = v;
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+__device__ __forceinline__ float half_max(float v) { float a, b; swap32_pair(v, a, b); return fmaxf(a, b); }
+__device__ __forceinline__ float half_sum(float v) { float a, b; swap32_pair(v, a, b); return a + b; }
 // max over the 4 lane groups of 16 (lane bits 4 and 5) with VALU permlane swaps, no LDS traffic
 __device__ __forceinline__ float group_max4(float v) {
-  const auto a = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-  v = fmaxf(__builtin_bit_cast(float, a[0]), __builtin_bit_cast(float, a[1]));
-  const auto b = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, v), __builtin_bit_cast(unsigned, v), false, false);
-  return fmaxf(__builtin_bit_cast(float, b[0]), __builtin_bit_cast(float, b[1]));
+  float a, b;
+  swap16_pair(v, a, b);
+  return half_max(fmaxf(a, b));
 }
 
 __device__ __forceinline__ uint4 ldg16(const void* p) { return *reinterpret_cast<const uint4*>(p); }

@@ -32,6 +32,8 @@ extern "C" int vda_debug_timestamps(void* host) {
 // halo-tiled 3x3 kernels (vda_depth.hip)
 int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
                    int BT, int H, int W, int C, hipStream_t st);
+int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st);
 int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
                   int Cout, hipStream_t st);
 
@@ -1242,6 +1244,16 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
   if (p.up_h > 0) return launch_reg_conv(p, (hipStream_t)stream);
+  // 3x3 convs with 256 output channels and Cin >= 512 on maps up to 160 wide (layer2..4_rn): strip-tiled
+  // halo kernel (vda_strip.hip; measured 10-14% faster there, 1-4% slower than the implicit GEMM at
+  // Cin = 256); vda_debug_force_tile(-3) routes every Cout = 256 conv to it, (-2) none
+  const bool strip_ok = g_force_tile == -3 || (g_force_tile == -1 && Cin >= 512);
+  if (strip_ok && ks == 3 && stride == 1 && pad == 1 && Cout == 256 && !p.epi.gamma && !p.epi.rowbias &&
+      (!p.epi.res || p.epi.ldres == Cout) && (!p.epi.res2 || p.epi.ldres2 == Cout)) {
+    rc = vda_conv_strip(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, BT, H, W,
+                        Cin, Cout, (hipStream_t)stream);
+    if (rc != 1) return rc;
+  }
   // large 3x3 maps with 128 output channels (output_conv1 at 296^2): halo-tiled kernel (vda_depth.hip)
   if (g_force_tile < 0 && ks == 3 && stride == 1 && pad == 1 && !pre_relu && !p.epi.res && !p.epi.res2 &&
       !p.epi.gamma && !p.epi.rowbias && (long)H * W >= 128L * 128L) {

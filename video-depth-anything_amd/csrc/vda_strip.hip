@@ -1,0 +1,222 @@
+// 3x3 / stride 1 / pad 1 convolutions with 256 output channels on maps up to 160 pixels wide (the
+// DPT head's layerN_rn convs and FeatureFusionBlock ResidualConvUnits at 148^2 / 74^2 / 37^2,
+// blocks.py:20-32, :68-91) as a halo-staged "strip" conv.
+//
+// A tile is 256 consecutive output pixels of one frame in row-major order (so no tile edge is wasted
+// on maps whose width is not a multiple of 16, e.g. 148 = 9.25 x 16).  Those pixels span at most
+// 3 image rows; the rows above and below plus one halo column each side (<= 5 x (W+2) pixels) are
+// staged ONCE per 32-channel slab by LDS-DMA and all 9 taps read them from LDS: input traffic ~2x the
+// map instead of the implicit GEMM's 9x.  Weights stream per (slab, tap) step (256 rows x 32 channels
+// = 16 KB) from L2.  Block = 8 waves, persistent; wave w: 4 m-blocks (64 pixels, mg = w & 3) x 8
+// n-blocks (128 channels, ng = w >> 2), 16x16x32 fp16 MFMA with W as the A operand (a lane owns 4
+// consecutive channels of one pixel).  Per step each wave issues 2 weight pieces and, on a slab's
+// first step, 7 pieces of the next slab's patch (fixed count: pieces past the patch reload the zero
+// page into spare slots), so every vmcnt is a constant; one raw s_barrier per step.
+// Epilogue: +bias, [ReLU], fp16 round, then + res + res2 as fp16 adds (the reference's fp16
+// residual adds, as in the GEMM epilogue); pre-ReLU (RCU, blocks.py:78) is applied to the X
+// fragments as they are read.
+#include "vda_common.h"
+#include "../../include/vda.h"
+
+namespace {
+
+__device__ __attribute__((aligned(64))) uint4 g_sz_page[4];
+
+constexpr int ST_M = 256;               // output pixels per tile
+constexpr int ST_SLAB = 32;             // channels per staged slab
+constexpr int ST_CPX = ST_SLAB / 8;     // 16-B chunks per pixel per slab (4)
+constexpr int ST_MAXW = 160;            // widest map served
+constexpr int ST_MAXPIX = 5 * (ST_MAXW + 2);                // patch pixels (<= 5 rows of W+2)
+constexpr int ST_PP = (ST_MAXPIX * ST_CPX + 63) / 64;       // 1-KiB pieces per patch slab (51)
+constexpr int ST_PPW = (ST_PP + 7) / 8;                     // per wave, fixed (7)
+constexpr int ST_PBUF = ST_PPW * 8 * 512;                   // halfs per patch ring slot (56 KiB)
+constexpr int ST_N = 256;                                   // output channels
+constexpr int ST_WBUF = ST_N * ST_CPX * 8;                  // halfs per weight step (16 KiB)
+
+struct StripParams {
+  const h16* x;
+  const h16* w;  // [256, 3, 3, Cin]
+  h16* y;
+  const float* bias;
+  const h16* res;
+  const h16* res2;
+  int H, W, Cin;
+  int pre_relu, relu_out;
+  int tiles_per_frame, ntiles;
+};
+
+__device__ __forceinline__ void st_glds16(const void* src, h16* lds_base) {
+  __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
+}
+template <int N>
+__device__ __forceinline__ void st_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ int st_ppos(int pp, int cd) { return cd ^ ((pp >> 1) & 3); }
+__device__ __forceinline__ int st_wpos(int n, int cd) { return cd ^ ((n >> 1) & 3); }
+
+__global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
+  __shared__ __attribute__((aligned(16))) h16 sm[2 * ST_PBUF + 2 * ST_WBUF];
+  h16* patch = sm;
+  h16* wbuf = sm + 2 * ST_PBUF;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mg = wave & 3, ng = wave >> 2;
+  const int W = p.W, H = p.H, HW = p.H * p.W, PW = p.W + 2;
+  const int nslab = p.Cin / ST_SLAB;
+  const int K = 9 * p.Cin;
+  const int my_tiles = (int)blockIdx.x < p.ntiles ? (p.ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int my_units = my_tiles * nslab;
+  if (my_units == 0) return;
+  const int my_steps = my_units * 9;
+  const void* zero = (const void*)g_sz_page;
+
+  auto tile_of_unit = [&](int u, int& bt, int& q0) {
+    const int t = (int)blockIdx.x + (u / nslab) * (int)gridDim.x;
+    bt = t / p.tiles_per_frame;
+    q0 = (t - bt * p.tiles_per_frame) * ST_M;
+  };
+  // patch of unit u -> ring slot (u & 1): image rows r0-1 .. r0-1+nrows-1, columns -1 .. W
+  auto dma_patch = [&](int u, int j) {
+    int bt, q0;
+    tile_of_unit(u, bt, q0);
+    const int slab = u % nslab;
+    const int r0 = q0 / W;
+    const int q1 = min(q0 + ST_M, HW) - 1;
+    const int npix = (q1 / W - r0 + 3) * PW;
+    const int q = wave + j * 8;  // piece index (fixed count per wave; pieces past the patch load zeros)
+    const int s = q * 64 + lane;
+    const int pp = s / ST_CPX, pos = s - pp * ST_CPX;
+    const int cd = st_ppos(pp, pos);
+    const int prow = pp / PW;
+    const int iy = r0 - 1 + prow, ix = pp - prow * PW - 1;
+    const void* src = zero;
+    if (pp < npix && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      src = p.x + (((long)bt * H + iy) * W + ix) * p.Cin + slab * ST_SLAB + cd * 8;
+    st_glds16(src, patch + (u & 1) * ST_PBUF + q * 512);
+  };
+  auto dma_w = [&](int gs) {
+    const int u = gs / 9, tap = gs - u * 9;
+    const int slab = u % nslab;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int piece = wave * 2 + j;
+      const int s = piece * 64 + lane;
+      const int n = s / ST_CPX, pos = s - n * ST_CPX;
+      const int cd = st_wpos(n, pos);
+      st_glds16(p.w + (long)n * K + tap * p.Cin + slab * ST_SLAB + cd * 8, wbuf + (gs & 1) * ST_WBUF + piece * 512);
+    }
+  };
+
+  for (int j = 0; j < ST_PPW; ++j) dma_patch(0, j);
+  dma_w(0);
+  st_wait<0>();
+  __builtin_amdgcn_s_barrier();
+
+  const int frow = lane & 15, g = lane >> 4;
+  f4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+  int pbase[4];  // patch pixel of this lane's output pixel for each m-block (tap (1,1) = centre)
+  int cur_tile_unit = -1;
+
+  for (int gs = 0; gs < my_steps; ++gs) {
+    const int u = gs / 9, tap = gs - u * 9;
+    if (gs + 1 < my_steps) dma_w(gs + 1);
+    const bool issue_p = tap == 0 && u + 1 < my_units;
+    if (issue_p)
+      for (int j = 0; j < ST_PPW; ++j) dma_patch(u + 1, j);
+    const int tu = u / nslab;
+    if (tu != cur_tile_unit) {  // new tile: per-lane patch coordinates of its 4 output pixels
+      cur_tile_unit = tu;
+      int bt, q0;
+      tile_of_unit(u, bt, q0);
+      const int r0 = q0 / W;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q = min(q0 + mg * 64 + i * 16 + frow, HW - 1);
+        const int r = q / W, c = q - r * W;
+        pbase[i] = (r - r0 + 1) * PW + c + 1;
+      }
+    }
+    const int dy = tap / 3, dx = tap - dy * 3;
+    const int toff = (dy - 1) * PW + (dx - 1);
+    const h16* pb = patch + (u & 1) * ST_PBUF;
+    const h16* wb = wbuf + (gs & 1) * ST_WBUF;
+    {
+      const int cd = g;
+      h8 xf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pp = pbase[i] + toff;
+        xf[i] = *reinterpret_cast<const h8*>(&pb[(pp * ST_CPX + st_ppos(pp, cd)) * 8]);
+        if (p.pre_relu) xf[i] = relu8(xf[i]);
+      }
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int n = (ng * 8 + a) * 16 + frow;
+        const h8 wf = *reinterpret_cast<const h8*>(&wb[(n * ST_CPX + st_wpos(n, cd)) * 8]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[a][i] = mfma16(wf, xf[i], acc[a][i]);
+      }
+    }
+    const bool tile_end = tap == 8 && (u % nslab) == nslab - 1;
+    if (tile_end) {
+      int bt, q0;
+      tile_of_unit(u, bt, q0);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        const int n = (ng * 8 + a) * 16 + g * 4;
+        const f4 bv = p.bias ? *reinterpret_cast<const f4*>(p.bias + n) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = q0 + mg * 64 + i * 16 + frow;
+          f4 v = acc[a][i] + bv;
+          acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+          if (q >= HW) continue;
+          h4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (h16)(p.relu_out ? fmaxf(v[r], 0.f) : v[r]);
+          const long off = ((long)bt * HW + q) * ST_N + n;
+          if (p.res) o += *reinterpret_cast<const h4*>(p.res + off);
+          if (p.res2) o += *reinterpret_cast<const h4*>(p.res2 + off);
+          *reinterpret_cast<h4*>(p.y + off) = o;
+        }
+      }
+    }
+    if (issue_p) st_wait<ST_PPW>();
+    else st_wait<0>();
+    __builtin_amdgcn_s_barrier();
+  }
+}
+
+int g_st_cus = 0;
+
+}  // namespace
+
+// Serves 3x3 / s1 / p1 convs with Cout == 256, Cin % 32 == 0, 16 <= W <= 160 (caller checks the
+// epilogue: bias, ReLU, res / res2 with row stride Cout).  Returns 1 when the shape is not served.
+int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st) {
+  if (Cout != ST_N || Cin % ST_SLAB != 0 || W > ST_MAXW || W < 16) return 1;
+  if (g_st_cus == 0) {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_st_cus = n > 0 ? n : 256;
+  }
+  StripParams p{};
+  p.x = (const h16*)x; p.w = (const h16*)w; p.y = (h16*)y; p.bias = bias;
+  p.res = (const h16*)res; p.res2 = (const h16*)res2;
+  p.H = H; p.W = W; p.Cin = Cin; p.pre_relu = pre_relu; p.relu_out = relu_out;
+  p.tiles_per_frame = (H * W + ST_M - 1) / ST_M;
+  const long nt = (long)BT * p.tiles_per_frame;
+  if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
+  p.ntiles = (int)nt;
+  const int grid = p.ntiles < g_st_cus ? p.ntiles : g_st_cus;
+  hipLaunchKernelGGL(strip_conv_kernel, dim3(grid), dim3(512), 0, st, p);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
