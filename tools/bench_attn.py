@@ -22,3 +22,13 @@ for _ in range(20): fn()
 e1.record(); torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / 20 * 1e3
 print(f"{'old' if os.environ.get('VDA_ATTN_OLD') else 'new'}: {us:.1f} us  {4 * B * H * N * N * D / us * 1e-6:.0f} TF/s  rel-L1 {err:.2e}", flush=True)
+for (S, C) in [(1369, 1024), (361, 1024), (1369, 256), (5476, 256)]:
+    T = 32
+    qkv = torch.randn(T * S, 3 * C, device="cuda", dtype=torch.float16)
+    fn = lambda: ops.temporal_attention(qkv, 1, T, S, 8, C // 8)
+    fn(); torch.cuda.synchronize()
+    e0.record()
+    for _ in range(10): fn()
+    e1.record(); torch.cuda.synchronize()
+    us = e0.elapsed_time(e1) / 10 * 1e3
+    print(f"temporal S={S} C={C}: {us:.1f} us  {T * S * C * 2 * 4 / us * 1e-3:.1f} GB/s", flush=True)
