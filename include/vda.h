@@ -230,6 +230,13 @@ int vda_debug_force_tile(int32_t cfg);
  */
 int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
 
+/*
+ * Tuning hook for the strip-tiled 3x3 conv: split every tile's input channels over nsplit work items
+ * (1, 2, 4, 8; must divide Cin / 32) whose fp32 partials are summed in a fixed order by a finishing
+ * kernel (0 = automatic, from a rounds x steps cost model).  Process-global; for tests and tuning.
+ */
+int vda_debug_strip_split(int32_t nsplit);
+
 #ifdef __cplusplus
 }
 #endif

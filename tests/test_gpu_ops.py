@@ -363,3 +363,42 @@ def test_conv3x3_strip_cout256(Cin, H, W, BT, mode):
     finally:
         lib.vda_debug_force_tile(-1)
     assert rel(y, y2) < 1e-3
+
+
+@pytest.mark.parametrize("Cin,H,W,BT,mode,split", [(1024, 19, 19, 4, "plain", 4), (256, 19, 19, 3, "rcu2", 4),
+                                                   (256, 19, 19, 2, "rcu1", 8), (512, 17, 23, 2, "rcu2", 2),
+                                                   (64, 19, 19, 2, "plain", 2), (256, 19, 19, 32, "rcu2", 0)])
+def test_conv3x3_strip_split(Cin, H, W, BT, mode, split):
+    """Strip conv with the input channels split over work items (fp32 partial slices summed in a
+    fixed order by the finishing kernel, which applies bias / ReLU / the fp16 residual adds): the
+    under-filled 19^2 maps (layer4_rn, refinenet4's RCU).  split 0 = the automatic choice.  vs torch
+    fp32, vs the unsplit kernel, and bit-identical across runs (no atomics)."""
+    x = rnd(BT, Cin, H, W, seed=190)
+    w, b = rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=191), rnd(256, scale=0.1, seed=192)
+    r1, r2 = rnd(BT, 256, H, W, seed=193), rnd(BT, 256, H, W, seed=194)
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    kw = {}
+    if mode == "plain":
+        ref = F.conv2d(x, w, padding=1)
+    elif mode == "rcu1":
+        ref = F.relu(F.conv2d(F.relu(x), w, b, padding=1))
+        kw = dict(bias=f32(b), pre_relu=True, act=ACT_RELU)
+    else:
+        ref = F.conv2d(x, w, b, padding=1) + r1 + r2
+        kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
+    ref = ref.permute(0, 2, 3, 1)
+    xh, wh = nh(x), nh(w)
+    lib = vda_amd._libvda()
+    lib.vda_debug_force_tile(-3)
+    try:
+        lib.vda_debug_strip_split(split)
+        y = ops.conv2d(xh, wh, **kw)
+        y_again = ops.conv2d(xh, wh, **kw)
+        lib.vda_debug_strip_split(1)
+        y1 = ops.conv2d(xh, wh, **kw)
+    finally:
+        lib.vda_debug_strip_split(0)
+        lib.vda_debug_force_tile(-1)
+    assert torch.equal(y, y_again)
+    assert rel(y, ref) < 2e-3
+    assert rel(y, y1) < 1e-3

@@ -1,0 +1,47 @@
+"""MFMA-busy fraction per kernel class from a rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE CSV.
+
+usage: python tools/pmc_mfma_summary.py <counter_collection.csv> <out.json> [n_cu]
+
+SQ_VALU_MFMA_BUSY_CYCLES sums, over every SIMD, the cycles its matrix core is busy (16 per
+v_mfma_f32_16x16x32_f16, 32 per 32x32x16: MI355X_MICROARCH.md, PMC units).  GRBM_GUI_ACTIVE is
+the kernel's GPU-busy cycles summed over the 8 XCDs, so kernel cycles = GRBM_GUI_ACTIVE / 8 and
+  mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (kernel cycles * n_cu * 4 SIMDs).
+The effective clock (kernel cycles / kernel wall time) is reported when the CSV carries timestamps;
+the guide notes it reads high on dispatches shorter than ~0.3 ms."""
+import csv, json, re, sys
+from collections import defaultdict
+
+path, out = sys.argv[1], sys.argv[2]
+n_cu = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+disp = defaultdict(dict)
+for r in csv.DictReader(open(path)):
+    d = disp[r["Dispatch_Id"]]
+    name = re.sub(r"\(anonymous namespace\)::", "", r["Kernel_Name"])
+    d["name"] = re.sub(r"\(.*", "", name)[:70]
+    d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    if "Start_Timestamp" in r and r.get("End_Timestamp"):
+        d["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+agg = defaultdict(lambda: {"dispatches": 0, "mfma_busy_cycles": 0.0, "kernel_cycles": 0.0, "ns": 0})
+for d in disp.values():
+    if "SQ_VALU_MFMA_BUSY_CYCLES" not in d or "GRBM_GUI_ACTIVE" not in d:
+        continue
+    a = agg[d["name"]]
+    a["dispatches"] += 1
+    a["mfma_busy_cycles"] += d["SQ_VALU_MFMA_BUSY_CYCLES"]
+    a["kernel_cycles"] += d["GRBM_GUI_ACTIVE"] / 8.0
+    a["ns"] += d.get("ns", 0)
+res = {"n_cu": n_cu, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * n_cu * 4)", "kernels": {}}
+tot_b = tot_c = 0.0
+for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["kernel_cycles"]):
+    busy = a["mfma_busy_cycles"] / max(1.0, a["kernel_cycles"] * n_cu * 4)
+    e = {"dispatches": a["dispatches"], "mfma_busy": round(busy, 4), "kernel_cycles": a["kernel_cycles"]}
+    if a["ns"]:
+        e["clock_ghz"] = round(a["kernel_cycles"] / a["ns"], 3)
+    res["kernels"][k] = e
+    tot_b += a["mfma_busy_cycles"]
+    tot_c += a["kernel_cycles"]
+res["all_kernels_mfma_busy"] = round(tot_b / max(1.0, tot_c * n_cu * 4), 4)
+json.dump(res, open(out, "w"), indent=1)
+for k, e in list(res["kernels"].items())[:14]:
+    print(f"{e['mfma_busy']:7.3f}  {e.get('clock_ghz', 0):5.2f} GHz  {e['dispatches']:5d}  {k}")
+print("all kernels", res["all_kernels_mfma_busy"])

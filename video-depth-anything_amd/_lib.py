@@ -20,7 +20,7 @@ EXPORTED = (
     "vda_depth_head", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
-    "vda_debug_force_tile", "vda_debug_gemm_sched",
+    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_strip_split",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -78,6 +78,7 @@ def _declare(lib):
         "vda_depth_head_f32": ([P, P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_debug_force_tile": ([I], I),
         "vda_debug_gemm_sched": ([I, I], I),
+        "vda_debug_strip_split": ([I], I),
     }
     for name, (args, res) in sig.items():
         if name.startswith("vda_debug_") and not hasattr(lib, name):

@@ -29,6 +29,13 @@ extern "C" int vda_debug_timestamps(void* host) {
 #endif
 #include "../../include/vda.h"
 
+// cache policy of the phased epilogue's output stores: nt (aux = 2).  In-situ A/B on one box
+// (tools/ab_libs.sh, 2 rounds): every phased GEMM/conv class 0.7-3.6 % faster, the forward's kernel
+// sum 55.77 -> 55.33 ms; the output tile is not re-read by the launch, so it need not stay in L2.
+#ifndef VDA_EPI_STORE_AUX
+#define VDA_EPI_STORE_AUX 2
+#endif
+
 // halo-tiled 3x3 kernels (vda_depth.hip)
 int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
                    int BT, int H, int W, int C, hipStream_t st);
@@ -990,7 +997,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
         if constexpr (NR >= 1) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, vr1 + it * sr1, 0, 0));
         if constexpr (NR >= 2) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, vr2 + it * sr2, 0, 0));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
       }
     };
     if (nres == 0) phase2(std::integral_constant<int, 0>{});
@@ -1247,7 +1254,10 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   // 3x3 convs with 256 output channels and Cin >= 512 on maps up to 160 wide (layer2..4_rn): strip-tiled
   // halo kernel (vda_strip.hip; measured 10-14% faster there, 1-4% slower than the implicit GEMM at
   // Cin = 256); vda_debug_force_tile(-3) routes every Cout = 256 conv to it, (-2) none
-  const bool strip_ok = g_force_tile == -3 || (g_force_tile == -1 && Cin >= 512);
+  // ... and any Cout = 256 3x3 conv whose 256-pixel strip tiles would fill at most half the CUs (19^2
+  // maps: the strip kernel then splits the input channels over several work items)
+  const long strip_tiles = (long)BT * ((H * W + 255) / 256);
+  const bool strip_ok = g_force_tile == -3 || (g_force_tile == -1 && (Cin >= 512 || strip_tiles * 2 <= cu_count()));
   if (strip_ok && ks == 3 && stride == 1 && pad == 1 && Cout == 256 && !p.epi.gamma && !p.epi.rowbias &&
       (!p.epi.res || p.epi.ldres == Cout) && (!p.epi.res2 || p.epi.ldres2 == Cout)) {
     rc = vda_conv_strip(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, BT, H, W,

@@ -27,33 +27,55 @@ __device__ __forceinline__ void ac_coord(int o, int in, int out, int& i0, int& i
   w = f - (float)i0;
 }
 
-// One thread per (output pixel, 8-channel chunk).
-__global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x, h16* __restrict__ y, int BT,
+// One block row per output row (bt, oy): the two source rows and the y weight are fixed per block,
+// and the (ox, 8-channel chunk) index within a row needs only 32-bit math.  (The first version
+// decomposed a flat 64-bit index per element: the 64-bit div/mod sequence held it at ~2.5 TB/s.)
+// Each thread writes UP x 16 B of the row, loads issued before any math.
+template <int UP>
+__global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x, h16* __restrict__ y, int rows,
                                                        int H, int W, int C, int Ho, int Wo) {
-  const int nch = C >> 3;
-  const long total = (long)BT * Ho * Wo * nch;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c = (int)(i % nch);
-    long t = i / nch;
-    const int ox = (int)(t % Wo); t /= Wo;
-    const int oy = (int)(t % Ho);
-    const int bt = (int)(t / Ho);
-    int y0, y1, x0, x1; float wy, wx;
+  const unsigned nch = (unsigned)C >> 3;
+  const unsigned row_items = (unsigned)Wo * nch;
+  const float sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+    const int bt = r / Ho, oy = r - bt * Ho;
+    int y0, y1; float wy;
     ac_coord(oy, H, Ho, y0, y1, wy);
-    ac_coord(ox, W, Wo, x0, x1, wx);
-    const h16* base = x + (long)bt * H * W * C + c * 8;
-    const h8 a = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * W + x0) * C));
-    const h8 bb = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * W + x1) * C));
-    const h8 cc = __builtin_bit_cast(h8, ldg16(base + ((long)y1 * W + x0) * C));
-    const h8 d = __builtin_bit_cast(h8, ldg16(base + ((long)y1 * W + x1) * C));
-    h8 o;
+    const h16* r0 = x + ((long)bt * H + y0) * W * C;
+    const h16* r1 = x + ((long)bt * H + y1) * W * C;
+    h16* out = y + (long)r * row_items * 8;
+    const unsigned step = gridDim.x * 256u;
+    for (unsigned i0 = blockIdx.x * 256u * UP + threadIdx.x; i0 < row_items; i0 += step * UP) {
+      h8 a[UP], b[UP], c[UP], d[UP];
+      float wx[UP];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float top = (1.f - wx) * (float)a[j] + wx * (float)bb[j];
-      const float bot = (1.f - wx) * (float)cc[j] + wx * (float)d[j];
-      o[j] = (h16)((1.f - wy) * top + wy * bot);
+      for (int u = 0; u < UP; ++u) {
+        const unsigned i = min(i0 + u * 256u, row_items - 1);
+        const unsigned ox = i / nch, ch = i - ox * nch;
+        const float f = sx * (float)ox;
+        const int x0 = (int)f, x1 = min(x0 + 1, W - 1);
+        wx[u] = f - (float)x0;
+        const unsigned o0 = (unsigned)x0 * C + ch * 8, o1 = (unsigned)x1 * C + ch * 8;
+        a[u] = __builtin_bit_cast(h8, ldg16(r0 + o0));
+        b[u] = __builtin_bit_cast(h8, ldg16(r0 + o1));
+        c[u] = __builtin_bit_cast(h8, ldg16(r1 + o0));
+        d[u] = __builtin_bit_cast(h8, ldg16(r1 + o1));
+      }
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        const unsigned i = i0 + u * 256u;
+        if (i < row_items) {
+          h8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float top = (1.f - wx[u]) * (float)a[u][j] + wx[u] * (float)b[u][j];
+            const float bot = (1.f - wx[u]) * (float)c[u][j] + wx[u] * (float)d[u][j];
+            o[j] = (h16)((1.f - wy) * top + wy * bot);
+          }
+          stg16(out + (long)i * 8, __builtin_bit_cast(uint4, o));
+        }
+      }
     }
-    stg16(y + i * 8, __builtin_bit_cast(uint4, o));
   }
 }
 
@@ -95,10 +117,14 @@ extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t
                                      int32_t Ho, int32_t Wo, void* stream) {
   VDA_CHECK_ARG(x && y, "null pointer");
   VDA_CHECK_ARG(BT > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && C > 0 && C % 8 == 0, "bad resize geometry");
-  const long total = (long)BT * Ho * Wo * (C / 8);
-  const int grid = (int)std::min<long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(upsample_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const h16*)x, (h16*)y, BT, H,
-                     W, C, Ho, Wo);
+  constexpr int UP = 2;
+  const long row_items = (long)Wo * (C / 8);
+  VDA_CHECK_ARG(row_items < (1L << 30) && (long)W * C < (1L << 31), "resize row too wide");
+  const int gx = (int)((row_items + 256 * UP - 1) / (256 * UP));
+  const int rows = BT * Ho;
+  const int gy = std::min(rows, 65535);
+  hipLaunchKernelGGL(upsample_kernel<UP>, dim3(gx, gy), dim3(256), 0, (hipStream_t)stream, (const h16*)x, (h16*)y,
+                     rows, H, W, C, Ho, Wo);
   VDA_LAUNCH_CHECK();
   return 0;
 }

@@ -1,5 +1,5 @@
 // 3x3 / stride 1 / pad 1 convolutions with 256 output channels on maps up to 160 pixels wide (the
-// DPT head's layerN_rn convs and FeatureFusionBlock ResidualConvUnits at 148^2 / 74^2 / 37^2,
+// DPT head's layerN_rn convs and FeatureFusionBlock ResidualConvUnits at 148^2 / 74^2 / 37^2 / 19^2,
 // blocks.py:20-32, :68-91) as a halo-staged "strip" conv.
 //
 // A tile is 256 consecutive output pixels of one frame in row-major order (so no tile edge is wasted
@@ -15,6 +15,12 @@
 // Epilogue: +bias, [ReLU], fp16 round, then + res + res2 as fp16 adds (the reference's fp16
 // residual adds, as in the GEMM epilogue); pre-ReLU (RCU, blocks.py:78) is applied to the X
 // fragments as they are read.
+//
+// Split over channel slabs: a small map has too few tiles for the chip (19^2 x 32 frames = 64 tiles
+// on 256 CUs: layer4_rn ran 310 us for 54 GFLOP).  A work item is then (tile, split): split s sums
+// slabs [s*nsl, (s+1)*nsl) and stores its fp32 partial tile into its own workspace slice with plain
+// stores; strip_finish_kernel adds the slices in a fixed order (deterministic) and applies the
+// epilogue.  The host picks the split count from a rounds x steps cost model (vda_conv_strip).
 #include "vda_common.h"
 #include "../../include/vda.h"
 
@@ -40,9 +46,12 @@ struct StripParams {
   const float* bias;
   const h16* res;
   const h16* res2;
+  float* ws;     // split > 1: [nsplit][BT * H * W][256] fp32 partial sums
+  long ws_slice; // BT * H * W * 256
   int H, W, Cin;
   int pre_relu, relu_out;
   int tiles_per_frame, ntiles;
+  int nsplit, nsl;  // channel-slab splits per tile, slabs per split
 };
 
 __device__ __forceinline__ void st_glds16(const void* src, h16* lds_base) {
@@ -63,24 +72,32 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mg = wave & 3, ng = wave >> 2;
   const int W = p.W, H = p.H, HW = p.H * p.W, PW = p.W + 2;
-  const int nslab = p.Cin / ST_SLAB;
+  const int nsl = p.nsl;                 // slabs per work item (all Cin / 32 when unsplit)
   const int K = 9 * p.Cin;
-  const int my_tiles = (int)blockIdx.x < p.ntiles ? (p.ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int my_units = my_tiles * nslab;
+  const int nitems = p.ntiles * p.nsplit;
+  const int my_items = (int)blockIdx.x < nitems ? (nitems - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int my_units = my_items * nsl;
   if (my_units == 0) return;
   const int my_steps = my_units * 9;
   const void* zero = (const void*)g_sz_page;
 
-  auto tile_of_unit = [&](int u, int& bt, int& q0) {
-    const int t = (int)blockIdx.x + (u / nslab) * (int)gridDim.x;
+  // unit u of this block -> work item (tile, split) -> frame bt, first pixel q0, split index
+  auto item_of_unit = [&](int u, int& bt, int& q0, int& sp) {
+    const int it = (int)blockIdx.x + (u / nsl) * (int)gridDim.x;
+    const int t = it / p.nsplit;
+    sp = it - t * p.nsplit;
     bt = t / p.tiles_per_frame;
     q0 = (t - bt * p.tiles_per_frame) * ST_M;
   };
+  auto slab_of_unit = [&](int u) {
+    const int it = (int)blockIdx.x + (u / nsl) * (int)gridDim.x;
+    return (it % p.nsplit) * nsl + u % nsl;
+  };
   // patch of unit u -> ring slot (u & 1): image rows r0-1 .. r0-1+nrows-1, columns -1 .. W
   auto dma_patch = [&](int u, int j) {
-    int bt, q0;
-    tile_of_unit(u, bt, q0);
-    const int slab = u % nslab;
+    int bt, q0, sp;
+    item_of_unit(u, bt, q0, sp);
+    const int slab = sp * nsl + u % nsl;
     const int r0 = q0 / W;
     const int q1 = min(q0 + ST_M, HW) - 1;
     const int npix = (q1 / W - r0 + 3) * PW;
@@ -97,7 +114,7 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
   };
   auto dma_w = [&](int gs) {
     const int u = gs / 9, tap = gs - u * 9;
-    const int slab = u % nslab;
+    const int slab = slab_of_unit(u);
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int piece = wave * 2 + j;
@@ -120,7 +137,7 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
   int pbase[4];  // patch pixel of this lane's output pixel for each m-block (tap (1,1) = centre)
-  int cur_tile_unit = -1;
+  int cur_item_unit = -1;
 
   for (int gs = 0; gs < my_steps; ++gs) {
     const int u = gs / 9, tap = gs - u * 9;
@@ -128,11 +145,11 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
     const bool issue_p = tap == 0 && u + 1 < my_units;
     if (issue_p)
       for (int j = 0; j < ST_PPW; ++j) dma_patch(u + 1, j);
-    const int tu = u / nslab;
-    if (tu != cur_tile_unit) {  // new tile: per-lane patch coordinates of its 4 output pixels
-      cur_tile_unit = tu;
-      int bt, q0;
-      tile_of_unit(u, bt, q0);
+    const int tu = u / nsl;
+    if (tu != cur_item_unit) {  // new work item: per-lane patch coordinates of its 4 output pixels
+      cur_item_unit = tu;
+      int bt, q0, sp;
+      item_of_unit(u, bt, q0, sp);
       const int r0 = q0 / W;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -162,27 +179,43 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
         for (int i = 0; i < 4; ++i) acc[a][i] = mfma16(wf, xf[i], acc[a][i]);
       }
     }
-    const bool tile_end = tap == 8 && (u % nslab) == nslab - 1;
-    if (tile_end) {
-      int bt, q0;
-      tile_of_unit(u, bt, q0);
+    const bool item_end = tap == 8 && (u % nsl) == nsl - 1;
+    if (item_end) {
+      int bt, q0, sp;
+      item_of_unit(u, bt, q0, sp);
+      if (p.nsplit > 1) {
+        // fp32 partial sums into this split's workspace slice (epilogue in strip_finish_kernel)
+        float* wsp = p.ws + (long)sp * p.ws_slice;
 #pragma unroll
-      for (int a = 0; a < 8; ++a) {
-        const int n = (ng * 8 + a) * 16 + g * 4;
-        const f4 bv = p.bias ? *reinterpret_cast<const f4*>(p.bias + n) : f4{0.f, 0.f, 0.f, 0.f};
+        for (int a = 0; a < 8; ++a) {
+          const int n = (ng * 8 + a) * 16 + g * 4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int q = q0 + mg * 64 + i * 16 + frow;
-          f4 v = acc[a][i] + bv;
-          acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
-          if (q >= HW) continue;
-          h4 o;
+          for (int i = 0; i < 4; ++i) {
+            const int q = q0 + mg * 64 + i * 16 + frow;
+            const f4 v = acc[a][i];
+            acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+            if (q < HW) *reinterpret_cast<f4*>(wsp + ((long)bt * HW + q) * ST_N + n) = v;
+          }
+        }
+      } else {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (h16)(p.relu_out ? fmaxf(v[r], 0.f) : v[r]);
-          const long off = ((long)bt * HW + q) * ST_N + n;
-          if (p.res) o += *reinterpret_cast<const h4*>(p.res + off);
-          if (p.res2) o += *reinterpret_cast<const h4*>(p.res2 + off);
-          *reinterpret_cast<h4*>(p.y + off) = o;
+        for (int a = 0; a < 8; ++a) {
+          const int n = (ng * 8 + a) * 16 + g * 4;
+          const f4 bv = p.bias ? *reinterpret_cast<const f4*>(p.bias + n) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int q = q0 + mg * 64 + i * 16 + frow;
+            f4 v = acc[a][i] + bv;
+            acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+            if (q >= HW) continue;
+            h4 o;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[r] = (h16)(p.relu_out ? fmaxf(v[r], 0.f) : v[r]);
+            const long off = ((long)bt * HW + q) * ST_N + n;
+            if (p.res) o += *reinterpret_cast<const h4*>(p.res + off);
+            if (p.res2) o += *reinterpret_cast<const h4*>(p.res2 + off);
+            *reinterpret_cast<h4*>(p.y + off) = o;
+          }
         }
       }
     }
@@ -192,9 +225,35 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
   }
 }
 
+// y = fp16([ReLU](sum_s ws[s] + bias)) + res + res2, 4 channels per thread, slices summed in order.
+__global__ __launch_bounds__(256) void strip_finish_kernel(const float* __restrict__ ws, int nsplit, long n4,
+                                                           const float* __restrict__ bias, int relu_out,
+                                                           const h16* __restrict__ res, const h16* __restrict__ res2,
+                                                           h16* __restrict__ y) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    f4 v = reinterpret_cast<const f4*>(ws)[i];
+    for (int s = 1; s < nsplit; ++s) v += reinterpret_cast<const f4*>(ws)[s * n4 + i];
+    if (bias) v += *reinterpret_cast<const f4*>(bias + ((int)i & (ST_N / 4 - 1)) * 4);
+    h4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (h16)(relu_out ? fmaxf(v[r], 0.f) : v[r]);
+    if (res) o += reinterpret_cast<const h4*>(res)[i];
+    if (res2) o += reinterpret_cast<const h4*>(res2)[i];
+    reinterpret_cast<h4*>(y)[i] = o;
+  }
+}
+
 int g_st_cus = 0;
+float* g_st_ws = nullptr;  // library-owned split workspace, grown on demand (one stream at a time)
+size_t g_st_ws_bytes = 0;
+int g_st_force_split = 0;  // tuning override (vda_debug_strip_split)
 
 }  // namespace
+
+extern "C" int vda_debug_strip_split(int32_t nsplit) {
+  g_st_force_split = nsplit;
+  return 0;
+}
 
 // Serves 3x3 / s1 / p1 convs with Cout == 256, Cin % 32 == 0, 16 <= W <= 160 (caller checks the
 // epilogue: bias, ReLU, res / res2 with row stride Cout).  Returns 1 when the shape is not served.
@@ -213,10 +272,46 @@ int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int
   p.H = H; p.W = W; p.Cin = Cin; p.pre_relu = pre_relu; p.relu_out = relu_out;
   p.tiles_per_frame = (H * W + ST_M - 1) / ST_M;
   const long nt = (long)BT * p.tiles_per_frame;
-  if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
+  if (nt > 0x7fffffffL / 8) return vda_set_error(-22, "conv: too many tiles");
   p.ntiles = (int)nt;
-  const int grid = p.ntiles < g_st_cus ? p.ntiles : g_st_cus;
+  // split count: minimise rounds x steps-per-item, charging a split its workspace round trip
+  // (s slices written + read, ~4 TB/s) in units of a ~1.1 us pipeline step
+  const int nslab = Cin / ST_SLAB;
+  const long M = (long)BT * H * W;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 8; s *= 2) {
+    if (nslab % s) continue;
+    const long items = nt * s;
+    const double rounds = (double)((items + g_st_cus - 1) / g_st_cus);
+    const double ws_us = s > 1 ? 2.0 * s * M * ST_N * 4 / 4e12 * 1e6 : 0.0;
+    const double cost = rounds * (nslab / s) * 9 + ws_us / 1.1;
+    if (cost < best_cost * 0.97) { best_cost = cost; best = s; }
+  }
+  if (g_st_force_split > 0 && nslab % g_st_force_split == 0) best = g_st_force_split;
+  p.nsplit = best;
+  p.nsl = nslab / best;
+  if (best > 1) {
+    const size_t need = (size_t)best * M * ST_N * sizeof(float);
+    if (need > g_st_ws_bytes) {
+      if (g_st_ws) (void)hipFree(g_st_ws);
+      g_st_ws = nullptr;
+      g_st_ws_bytes = 0;
+      if (hipMalloc(&g_st_ws, need) != hipSuccess) return vda_set_error(-12, "conv: split workspace allocation failed");
+      g_st_ws_bytes = need;
+    }
+    p.ws = g_st_ws;
+    p.ws_slice = M * ST_N;
+  }
+  const long nitems = nt * best;
+  const int grid = (int)(nitems < g_st_cus ? nitems : g_st_cus);
   hipLaunchKernelGGL(strip_conv_kernel, dim3(grid), dim3(512), 0, st, p);
+  if (best > 1) {
+    const long n4 = M * ST_N / 4;
+    const int fg = (int)std::min<long>((n4 + 255) / 256, 4096);
+    hipLaunchKernelGGL(strip_finish_kernel, dim3(fg), dim3(256), 0, st, (const float*)g_st_ws, best, n4, bias, relu_out,
+                       (const h16*)res, (const h16*)res2, (h16*)y);
+  }
   VDA_LAUNCH_CHECK();
   return 0;
 }
