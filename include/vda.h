@@ -218,7 +218,8 @@ int vda_depth_head_f32(const float* x, const float* w1, const float* b1, const f
 /*
  * Tuning hook: force the GEMM/conv tile configuration (-1 = automatic; 0 = 128x128/4 waves,
  * 1 = 256x128/8 waves, 2 = 128x64/4 waves, 3 = 256x256/8 waves; -2 / -3 = automatic tiles with the
- * strip-tiled 3x3 conv for no / every Cout = 256 shape; 10 + cfg = implicit-GEMM depth tail).
+ * strip-tiled 3x3 conv for no / every Cout = 256 shape; 9 = depth tail on a materialised resize
+ * instead of the resize fused into the halo conv; 10 + cfg = implicit-GEMM depth tail).
  * Process-global; for benchmarks and tests.
  */
 int vda_debug_force_tile(int32_t cfg);

@@ -402,3 +402,54 @@ def test_conv3x3_strip_split(Cin, H, W, BT, mode, split):
     assert torch.equal(y, y_again)
     assert rel(y, ref) < 2e-3
     assert rel(y, y1) < 1e-3
+
+
+@pytest.mark.parametrize("C,Hin,Win,Ho,Wo,BT", [(128, 20, 24, 37, 51, 2), (64, 9, 9, 16, 16, 1), (128, 37, 37, 70, 70, 3),
+                                                 (64, 30, 17, 53, 31, 2), (128, 12, 12, 12, 12, 1), (64, 5, 40, 33, 47, 1)])
+def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
+    """Depth tail with the bilinear resize fused into the halo conv's patch staging (the default for
+    C % 64 == 0): bit-identical to the materialised resize + halo conv (vda_debug_force_tile(9)),
+    both interpolating with the same fp32 formula and fp16 rounding; partial tiles, non-square maps,
+    identity-size resize, aspect ratios far from 1."""
+    x = rnd(BT, C, Hin, Win, seed=145)
+    b1 = rnd(32, scale=0.1, seed=147)
+    w2, b2 = rnd(1, 32, 1, 1, seed=148).abs() * 0.2, torch.tensor([0.05])
+    w1 = torch.randn(32, C, 3, 3, generator=torch.Generator().manual_seed(146)) * (9 * C) ** -0.5
+    xh = h(x.permute(0, 2, 3, 1))
+    up = F.interpolate(xh.float().cpu().permute(0, 3, 1, 2), size=(Ho, Wo), mode="bilinear", align_corners=True)
+    ref = F.relu(F.conv2d(F.relu(F.conv2d(up.half().float(), w1, b1, padding=1)), w2, b2))[:, 0]
+    wn = w1.permute(0, 2, 3, 1)
+    split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0).to(DEV).contiguous()
+    args = (split, f32(b1), f32(w2.reshape(-1)), f32(b2), Ho, Wo)
+    y = ops.depth_head(xh, *args)
+    lib = vda_amd._libvda()
+    lib.vda_debug_force_tile(9)
+    try:
+        y_mat = ops.depth_head(xh, *args)
+    finally:
+        lib.vda_debug_force_tile(-1)
+    assert torch.equal(y, y_mat)
+    assert rel(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize("BT,Cin,Hs,Ws,H,W,relu", [(2, 256, 70, 70, 140, 140, False), (2, 128, 64, 72, 128, 143, True),
+                                                   (1, 64, 20, 150, 39, 299, False), (3, 128, 9, 9, 17, 17, False)])
+def test_conv3x3_halo_fused_resize(BT, Cin, Hs, Ws, H, W, relu):
+    """output_conv1 shape class (3x3, Cout = 128) on a bilinear align_corners=True resize fused into the
+    halo conv's patch staging: vs torch fp32, and bit-identical to resize + halo conv when the
+    materialised path also takes the halo kernel (resized maps >= 128^2)."""
+    x = rnd(BT, Cin, Hs, Ws, seed=170)
+    w = rnd(128, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=171)
+    b = rnd(128, scale=0.1, seed=172)
+    xh = h(x.permute(0, 2, 3, 1))
+    up = F.interpolate(xh.float().cpu().permute(0, 3, 1, 2), size=(H, W), mode="bilinear", align_corners=True)
+    ref = F.conv2d(up.half().float(), w, b, padding=1)
+    if relu:
+        ref = F.relu(ref)
+    kw = dict(bias=f32(b), act=ACT_RELU if relu else 0)
+    wh = h(w.permute(0, 2, 3, 1))
+    y = ops.conv2d(xh, wh, up=(H, W), **kw)
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 2e-3
+    if H * W >= 128 * 128:
+        y_mat = ops.conv2d(ops.upsample_bilinear(xh, H, W), wh, **kw)
+        assert torch.equal(y, y_mat)

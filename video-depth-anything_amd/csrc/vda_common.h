@@ -54,6 +54,20 @@ __device__ __forceinline__ float erf_fast(float x) {
   const float r = fmaf(-y, e, 1.0f);
   return copysignf(r, x);
 }
+// Bilinear blend of 8 fp16 channels in fp32, rounded to fp16: (1-wy)*((1-wx)*a + wx*b) + wy*((1-wx)*c + wx*d)
+// with every product / fma spelled out, so the resize kernel and the depth head's fused patch builder
+// produce bit-identical values (no compiler contraction choices in between).
+__device__ __forceinline__ h8 bilerp8(h8 a, h8 b, h8 c, h8 d, float wx, float wy) {
+  const float ux = 1.f - wx, uy = 1.f - wy;
+  h8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float top = __builtin_fmaf(wx, (float)b[j], ux * (float)a[j]);
+    const float bot = __builtin_fmaf(wx, (float)d[j], ux * (float)c[j]);
+    o[j] = (h16)__builtin_fmaf(wy, bot, uy * top);
+  }
+  return o;
+}
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }

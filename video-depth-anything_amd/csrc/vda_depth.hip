@@ -46,16 +46,35 @@ template <int CPX>
 __device__ __forceinline__ int w_pos(int n, int cd) {
   return cd ^ ((n >> 1) & (CPX - 1));
 }
+// align_corners=True source coordinate, as vda_upsample_bilinear computes it (torch upsample_bilinear2d);
+// sc = (in - 1) / (out - 1) (0 for out == 1) is hoisted out by the caller, same float division
+__device__ __forceinline__ float dh_ac_scale(int in, int out) {
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+}
+__device__ __forceinline__ void dh_ac_coord(int o, int in, float sc, int& i0, int& i1, float& w) {
+  const float f = sc * (float)o;
+  i0 = (int)f;
+  i1 = min(i0 + 1, in - 1);
+  w = f - (float)i0;
+}
 
 // DEPTH: the depth tail (64 weight rows = 32 hi + 32 lo, wave n-blocks {ng, ng+2}, ReLU/1x1/ReLU epilogue
 // to fp32 depth).  !DEPTH: a plain 3x3 conv with NROW output channels (wave n-blocks ng*NB4 .. +NB4-1,
 // epilogue +bias [ReLU] -> fp16 NHWC).  TPS taps per pipeline step (3 = one kernel row, or 1).
-template <int SLAB, int NROW, int TPS, bool DEPTH>
+// UPS: U is the [BT, Hs, Ws, C] map BEFORE the bilinear (align_corners=True) resize to (H, W), and the
+// patch is interpolated instead of copied, so the resized map is never written to HBM.  The source
+// region a tile's 18x18 patch needs (<= 12 x 12 pixels for a scale <= 0.6) is staged ONCE per slab by
+// LDS-DMA in place of the patch (same fixed-count piece scheme, 3 pieces per wave, one slot: it is
+// filled at a unit's first step and consumed at its last), and at the unit's last step every thread
+// interpolates its 16-B patch slots from LDS in fp32 (bilerp8: the resize kernel's formula and
+// op order, so the fp16 values are bit-identical) into the other patch ring slot.
+template <int SLAB, int NROW, int TPS, bool DEPTH, bool UPS = false>
 __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ w2,
                                                         const float* __restrict__ b2, float* __restrict__ depth,
                                                         h16* __restrict__ yout, int relu_out,
-                                                        int H, int W, int C, int tiles_x, int tiles_y, int ntiles) {
+                                                        int H, int W, int C, int tiles_x, int tiles_y, int ntiles,
+                                                        int Hs = 0, int Ws = 0) {
   static_assert(!DEPTH || NROW == 64, "depth tail: 64 weight rows");
   constexpr int NB = NROW / 32;                          // n-blocks per wave (2 for the depth tail)
   constexpr int CPX = SLAB / 8;                          // 16-B chunks per pixel per slab
@@ -68,10 +87,15 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   constexpr int WPCS = WSLOT / 64;                       // weight pieces per step (24 or 12)
   constexpr int WPW = (WPCS + 7) / 8;                    // per wave (3 or 2; surplus waves duplicate)
   constexpr int ND = SLAB / 32;                          // MFMA k-depths per tap
-  __shared__ __attribute__((aligned(16))) h16 dsm[2 * PBUF + 2 * WBUF + 512];
+  constexpr int WRING = 2;                               // weight ring
+  static_assert(!UPS || (CPX == 8 && 9 / TPS >= 2), "UPS: 64-channel slabs, >= 2 steps per unit");
+  constexpr int SPPW = 3;                                // UPS source pieces per wave (fixed count)
+  constexpr int SSLOT = UPS ? SPPW * 8 * 64 : 0;         // source slots: 1536 = 192 pixels x 8 chunks
+  __shared__ __attribute__((aligned(16))) h16 dsm[2 * PBUF + WRING * WBUF + SSLOT * 8 + 512];
   h16* patch = dsm;                                      // [2][PBUF]
-  h16* wbuf = dsm + 2 * PBUF;                            // [2][WBUF]
-  float* scratch = reinterpret_cast<float*>(dsm + 2 * PBUF + 2 * WBUF);  // [256]
+  h16* wbuf = dsm + 2 * PBUF;                            // [WRING][WBUF]
+  h16* sbuf = dsm + 2 * PBUF + WRING * WBUF;             // [SSLOT * 8] (UPS)
+  float* scratch = reinterpret_cast<float*>(dsm + 2 * PBUF + WRING * WBUF + SSLOT * 8);  // [256]
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -112,6 +136,59 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     dh_glds16(src, patch + (u & 1) * PBUF + q * 512);
   };
   // weight pieces of global step gs (kernel row dy of slab) -> ring slot (gs & 1)
+  // UPS: source region of unit u's patch: rows sy_lo .. sy_lo + SR - 1, columns sx_lo .. + SC - 1
+  constexpr int USL = DNPIX * CPX;                       // 16-B patch slots read by the taps
+  constexpr int UCH = UPS ? (USL + 511) / 512 : 1;       // patch slots per thread
+  const float usy = UPS ? dh_ac_scale(Hs, H) : 0.f, usx = UPS ? dh_ac_scale(Ws, W) : 0.f;
+  auto src_region = [&](int y0, int x0, int& sy_lo, int& sx_lo, int& SR, int& SC) {
+    sy_lo = (int)(usy * (float)max(y0 - 1, 0));
+    sx_lo = (int)(usx * (float)max(x0 - 1, 0));
+    SR = min((int)(usy * (float)min(y0 + DT, H - 1)) + 1, Hs - 1) - sy_lo + 1;
+    SC = min((int)(usx * (float)min(x0 + DT, W - 1)) + 1, Ws - 1) - sx_lo + 1;
+  };
+  // piece j (of SPPW) of unit u's source region -> sbuf; slot = pixel * 8 + chunk
+  auto dma_src = [&](int u, int j) {
+    int bt, y0, x0, sy_lo, sx_lo, SR, SC;
+    tile_of_unit(u, bt, y0, x0);
+    src_region(y0, x0, sy_lo, sx_lo, SR, SC);
+    const int slab = u % units_per_tile;
+    const int q = wave + j * 8;
+    const int s = q * 64 + lane;
+    const int px = s >> 3, cd = s & 7;
+    const int r = px / SC, c = px - r * SC;
+    const void* src = zero;
+    if (r < SR) src = U + (((long)bt * Hs + sy_lo + r) * Ws + sx_lo + c) * C + slab * SLAB + cd * 8;
+    dh_glds16(src, sbuf + q * 512);
+  };
+  // interpolate unit u's patch from sbuf into patch ring slot (u & 1); padding pixels -> 0
+  auto ups_interp = [&](int u) {
+    int bt, y0, x0, sy_lo, sx_lo, SR, SC;
+    tile_of_unit(u, bt, y0, x0);
+    src_region(y0, x0, sy_lo, sx_lo, SR, SC);
+#pragma unroll
+    for (int k = 0; k < UCH; ++k) {
+      const int s = tid + k * 512;
+      const int sc = min(s, USL - 1);
+      const int p = sc / CPX, pos = sc - p * CPX;
+      const int cd = patch_pos<CPX>(p, pos);
+      const int pr = p / DP;
+      const int py = y0 - 1 + pr, px = x0 - 1 + (p - pr * DP);
+      const bool ok = (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W;
+      int sy0, sy1, sx0, sx1;
+      float wy, wx;
+      dh_ac_coord(min(max(py, 0), H - 1), Hs, usy, sy0, sy1, wy);
+      dh_ac_coord(min(max(px, 0), W - 1), Ws, usx, sx0, sx1, wx);
+      const int r0 = (sy0 - sy_lo) * SC, r1 = (sy1 - sy_lo) * SC, c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
+      const h8 a = *reinterpret_cast<const h8*>(sbuf + ((r0 + c0) * 8 + cd) * 8);
+      const h8 b = *reinterpret_cast<const h8*>(sbuf + ((r0 + c1) * 8 + cd) * 8);
+      const h8 c = *reinterpret_cast<const h8*>(sbuf + ((r1 + c0) * 8 + cd) * 8);
+      const h8 d = *reinterpret_cast<const h8*>(sbuf + ((r1 + c1) * 8 + cd) * 8);
+      const h8 v = bilerp8(a, b, c, d, wx, wy);
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+      const uint4 o = ok ? __builtin_bit_cast(uint4, v) : z;
+      if (k + 1 < UCH || s < USL) *reinterpret_cast<uint4*>(patch + (u & 1) * PBUF + s * 8) = o;
+    }
+  };
   auto dma_w = [&](int gs) {
     const int u = gs / SPU, st = gs - u * SPU;
     const int slab = u % units_per_tile;
@@ -127,9 +204,18 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   };
 
   // prologue: patch of unit 0 (all pieces, split over waves) + weights of step 0
-  for (int q = wave; q < PP; q += 8) dma_patch(0, q);
-  dma_w(0);
-  dh_wait_vmcnt<0>();
+  if constexpr (UPS) {
+    for (int j = 0; j < SPPW; ++j) dma_src(0, j);
+    dma_w(0);
+    dh_wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    ups_interp(0);
+    __syncthreads();  // patch slot 0 written, source slot free for unit 1
+  } else {
+    for (int q = wave; q < PP; q += 8) dma_patch(0, q);
+    dma_w(0);
+    dh_wait_vmcnt<0>();
+  }
   __builtin_amdgcn_s_barrier();
 
   const int frow = lane & 15, g = lane >> 4;
@@ -149,10 +235,18 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     // weights of the next step first, then (first step of a unit) the whole next patch slab: the
     // end-of-step wait then leaves exactly the patch pieces in flight, and they land by the end of
     // the unit's second step
-    if (gs + 1 < my_steps) dma_w(gs + 1);
     const bool issue_p = st == 0 && u + 1 < my_units;
-    if (issue_p)
+    if (gs + 1 < my_steps) dma_w(gs + 1);
+    if constexpr (UPS) {
+      // first step: the next unit's source region (lands by the end of the second step); last step:
+      // interpolate the next unit's patch from it into the other patch slot (published by this
+      // step's barrier; the source slot is refilled only after it)
+      if (issue_p)
+        for (int j = 0; j < SPPW; ++j) dma_src(u + 1, j);
+      if (st == SPU - 1 && u + 1 < my_units) ups_interp(u + 1);
+    } else if (issue_p) {
       for (int j = 0; j < my_pp; ++j) dma_patch(u + 1, wave + j * 8);
+    }
     // ---- TPS taps x ND k-depths x (NB x 4) MFMAs
     const h16* pb = patch + (u & 1) * PBUF;
     const h16* wb = wbuf + (gs & 1) * WBUF;
@@ -223,7 +317,10 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       }
       tile_of_unit(u, pend_bt, pend_y0, pend_x0);
     }
-    if (issue_p) {
+    if constexpr (UPS) {
+      if (issue_p) dh_wait_vmcnt<SPPW>();
+      else dh_wait_vmcnt<0>();
+    } else if (issue_p) {
       if (my_pp == PPMAX) dh_wait_vmcnt<PPMAX>();
       else dh_wait_vmcnt<PPMAX - 1>();
     } else {
@@ -270,6 +367,58 @@ int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* 
   else
     hipLaunchKernelGGL((halo_conv_kernel<64, 64, 3, true>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1,
                        b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+// Depth tail straight from the UN-resized output_conv1 map x [BT, Hs, Ws, C] (C % 64 == 0, Hs <= H,
+// Ws <= W): the bilinear resize is computed while the halo patch is built (UPS), so the resized map
+// (2.2 GB at ViT-L 32x518^2) is never written.  Returns 1 when the shape is not served.
+int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
+                         float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st) {
+  if (C % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return 1;
+  // the staged source region of a tile (<= floor(17 * scale) + 2 rows / columns) must fit 192 pixels
+  const float sy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f, sx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
+  if (((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) > 192) return 1;
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = n > 0 ? n : 256;
+  }
+  const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
+  const long nt = (long)BT * tiles_x * tiles_y;
+  if (nt > 0x7fffffffL) return vda_set_error(-22, "depth head: too many tiles");
+  const int ntiles = (int)nt;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((halo_conv_kernel<64, 64, 3, true, true>), dim3(grid), dim3(512), 0, st, (const h16*)x,
+                     (const h16*)w1, b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+// output_conv1 on the 2x resize of refinenet1's output without writing the resized map: the halo conv
+// below with the resize fused into its patch staging (UPS).  x [BT, Hs, Ws, Cin] is the map BEFORE the
+// bilinear (align_corners=True) resize to (H, W).  Returns 1 when the shape is not served.
+int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int Hs, int Ws,
+                        int H, int W, int Cin, int Cout, hipStream_t st) {
+  if (Cout != 128 || Cin % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return 1;
+  const float sy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f, sx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
+  if (((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) > 192) return 1;
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_num_cus = n > 0 ? n : 256;
+  }
+  const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
+  const long nt = (long)BT * tiles_x * tiles_y;
+  if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
+  const int ntiles = (int)nt;
+  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false, true>), dim3(grid), dim3(512), 0, st, (const h16*)x,
+                     (const h16*)w, bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu,
+                     H, W, Cin, tiles_x, tiles_y, ntiles, Hs, Ws);
   VDA_LAUNCH_CHECK();
   return 0;
 }

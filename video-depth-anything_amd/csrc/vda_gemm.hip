@@ -43,6 +43,10 @@ int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int
                    const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st);
 int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
                   int Cout, hipStream_t st);
+int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
+                         float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st);
+int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int Hs, int Ws,
+                        int H, int W, int Cin, int Cout, hipStream_t st);
 
 namespace {
 
@@ -1250,7 +1254,17 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
                 "conv: row store, activation none/relu");
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
-  if (p.up_h > 0) return launch_reg_conv(p, (hipStream_t)stream);
+  if (p.up_h > 0) {
+    // 3x3 conv on a bilinear resize with 128 outputs (output_conv1 on refinenet1's x2 resize): the
+    // halo conv with the resize fused into its patch staging (bit-identical to resize + conv)
+    if (g_force_tile < 0 && ks == 3 && stride == 1 && pad == 1 && !pre_relu && !p.epi.res && !p.epi.res2 &&
+        !p.epi.gamma && !p.epi.rowbias) {
+      rc = vda_conv_halo_fused(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, BT, H, W, p.up_h, p.up_w, Cin, Cout,
+                               (hipStream_t)stream);
+      if (rc != 1) return rc;
+    }
+    return launch_reg_conv(p, (hipStream_t)stream);
+  }
   // 3x3 convs with 256 output channels and Cin >= 512 on maps up to 160 wide (layer2..4_rn): strip-tiled
   // halo kernel (vda_strip.hip; measured 10-14% faster there, 1-4% slower than the implicit GEMM at
   // Cin = 256); vda_debug_force_tile(-3) routes every Cout = 256 conv to it, (-2) none
@@ -1281,9 +1295,16 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   VDA_CHECK_ARG(BT > 0 && Hin > 0 && Win > 0 && Ho > 0 && Wo > 0, "bad depth-head geometry");
   VDA_CHECK_ARG(C % 8 == 0, "depth head needs C % 8 == 0");
   hipStream_t st = (hipStream_t)stream;
+  int rc;
+  // 0) default: resize fused into the halo conv's patch staging (the resized map is never written;
+  //    bit-identical to 1 + 2).  vda_debug_force_tile(9) takes the materialised path below.
+  if (g_force_tile < 9) {
+    rc = vda_depth_halo_fused(x, w1, b1, w2, b2, depth, BT, Hin, Win, Ho, Wo, C, st);
+    if (rc != 1) return rc;
+  }
   // 1) bilinear (align_corners=True) resize of the output_conv1 map to (Ho, Wo), fp16 like the
   //    reference's autocast interpolate (dpt_temporal.py:92-94)
-  int rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
+  rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
   if (rc) return rc;
   // 2) 3x3 conv C -> 32 with split-fp16 weights + fused ReLU / 1x1 / ReLU epilogue: the halo-tiled
   //    kernel (vda_depth.hip) unless a tuning override asks for the implicit-GEMM one

@@ -244,8 +244,12 @@ __global__ __launch_bounds__(256) void strip_finish_kernel(const float* __restri
 }
 
 int g_st_cus = 0;
-float* g_st_ws = nullptr;  // library-owned split workspace, grown on demand (one stream at a time)
-size_t g_st_ws_bytes = 0;
+// Split workspace: a static device buffer (allocated with the code object, so no entry point
+// allocates device memory and split convs stay capturable in a hipGraph).  96 MiB covers ViT-L 32 x
+// 19^2 (and 19 x 33 at 518 x 924) in 4 splits; a split that would not fit is not chosen.  Library-
+// global: callers must not run split convs concurrently on two streams.
+constexpr long ST_WS_FLOATS = 24L << 20;
+__device__ float g_st_ws[ST_WS_FLOATS];
 int g_st_force_split = 0;  // tuning override (vda_debug_strip_split)
 
 }  // namespace
@@ -281,26 +285,22 @@ int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int
   int best = 1;
   double best_cost = 1e30;
   for (int s = 1; s <= 8; s *= 2) {
-    if (nslab % s) continue;
+    if (nslab % s || (s > 1 && (long)s * M * ST_N > ST_WS_FLOATS)) continue;
     const long items = nt * s;
     const double rounds = (double)((items + g_st_cus - 1) / g_st_cus);
     const double ws_us = s > 1 ? 2.0 * s * M * ST_N * 4 / 4e12 * 1e6 : 0.0;
     const double cost = rounds * (nslab / s) * 9 + ws_us / 1.1;
     if (cost < best_cost * 0.97) { best_cost = cost; best = s; }
   }
-  if (g_st_force_split > 0 && nslab % g_st_force_split == 0) best = g_st_force_split;
+  if (g_st_force_split > 0 && nslab % g_st_force_split == 0 && (long)g_st_force_split * M * ST_N <= ST_WS_FLOATS)
+    best = g_st_force_split;
   p.nsplit = best;
   p.nsl = nslab / best;
+  float* ws = nullptr;
   if (best > 1) {
-    const size_t need = (size_t)best * M * ST_N * sizeof(float);
-    if (need > g_st_ws_bytes) {
-      if (g_st_ws) (void)hipFree(g_st_ws);
-      g_st_ws = nullptr;
-      g_st_ws_bytes = 0;
-      if (hipMalloc(&g_st_ws, need) != hipSuccess) return vda_set_error(-12, "conv: split workspace allocation failed");
-      g_st_ws_bytes = need;
-    }
-    p.ws = g_st_ws;
+    if (hipGetSymbolAddress((void**)&ws, HIP_SYMBOL(g_st_ws)) != hipSuccess || !ws)
+      return vda_set_error(-22, "conv: split workspace symbol unavailable");
+    p.ws = ws;
     p.ws_slice = M * ST_N;
   }
   const long nitems = nt * best;
@@ -309,7 +309,7 @@ int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int
   if (best > 1) {
     const long n4 = M * ST_N / 4;
     const int fg = (int)std::min<long>((n4 + 255) / 256, 4096);
-    hipLaunchKernelGGL(strip_finish_kernel, dim3(fg), dim3(256), 0, st, (const float*)g_st_ws, best, n4, bias, relu_out,
+    hipLaunchKernelGGL(strip_finish_kernel, dim3(fg), dim3(256), 0, st, (const float*)ws, best, n4, bias, relu_out,
                        (const h16*)res, (const h16*)res2, (h16*)y);
   }
   VDA_LAUNCH_CHECK();

@@ -543,8 +543,12 @@ class VideoDepthAnything(nn.Module):
         p2 = ops.upsample_bilinear(y, r1.shape[1], r1.shape[2])
         y, _ = self._fusion(P.ref[1], p2, r1, None)  # refinenet1: scale_factor 2
         H1, W1 = 2 * y.shape[1], 2 * y.shape[2]
-        # refinenet1's x2 bilinear upsample (blocks.py:151-158) materialised once, then output_conv1
-        o1 = ops.conv2d(ops.upsample_bilinear(y, H1, W1), P.oc1_w, bias=P.oc1_b)
+        # refinenet1's x2 bilinear upsample (blocks.py:151-158) fused into output_conv1's patch staging
+        # (fp16: the halo conv builds each patch by interpolation; fp32 mode materialises the resize)
+        if P.fp32:
+            o1 = ops.conv2d(ops.upsample_bilinear(y, H1, W1), P.oc1_w, bias=P.oc1_b)
+        else:
+            o1 = ops.conv2d(y, P.oc1_w, bias=P.oc1_b, up=(H1, W1))
         # output_conv2 with fp32 weights on the bilinear resize to (14ph, 14pw) (dpt_temporal.py:92-97);
         # the final resize to (H, W) is the identity because H = 14ph, W = 14pw (video_depth.py:63)
         if P.fp32:
