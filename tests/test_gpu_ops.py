@@ -157,7 +157,7 @@ def test_conv3x3_fused_upsample():
     assert rel(y, ref.permute(0, 2, 3, 1)) < 3e-3
 
 
-@pytest.mark.parametrize("C", [384, 1024, 256, 64])
+@pytest.mark.parametrize("C", [384, 1024, 256, 64, 128, 512])
 def test_layernorm(C):
     R = 517
     x = rnd(R, C, seed=30) * 2 + 0.5
@@ -166,8 +166,9 @@ def test_layernorm(C):
     assert rel(y, F.layer_norm(x, (C,), g, b, eps=1e-6)) < 2e-3
 
 
-def test_layernorm_skip_cls():
-    BT, np_, C = 3, 10, 384
+@pytest.mark.parametrize("C", [384, 256])
+def test_layernorm_skip_cls(C):
+    BT, np_ = 3, 10
     x = rnd(BT, np_ + 1, C, seed=33)
     g, b = rnd(C, seed=34) * 0.1 + 1, rnd(C, seed=35) * 0.1
     y = ops.layernorm(h(x.reshape(-1, C)), f32(g), f32(b), 1e-6, skip_period=np_)

@@ -59,6 +59,44 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const h16* __restrict__ 
   }
 }
 
+// Narrow rows (C <= 512, the motion modules' C = 256 / 128): one wave would leave lanes idle and
+// wait on one 512-B row, so LPR = C / 8 lanes own a row (one 16-B chunk each) and a wave normalises
+// 64 / LPR rows; the same two-pass statistics, reduced over the row's LPR lanes only.
+template <int LPR>
+__global__ __launch_bounds__(256) void layernorm_narrow_kernel(const h16* __restrict__ x, long ldx,
+                                                               h16* __restrict__ y, const float* __restrict__ g,
+                                                               const float* __restrict__ b, int rows, int C,
+                                                               float eps, int skip_period) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane / LPR, c = lane % LPR;
+  const int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + sub;
+  const bool ok = row < rows;
+  const int r = ok ? row : rows - 1;  // every lane joins the shuffles
+  const long src_row = skip_period > 0 ? (long)r + r / skip_period + 1 : (long)r;
+  const h8 t = __builtin_bit_cast(h8, ldg16(x + src_row * ldx + c * 8));
+  float v[8], s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { v[j] = (float)t[j]; s += v[j]; }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { const float d = v[j] - mean; q += d * d; }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = rsqrtf(q / (float)C + eps);
+  const f4 g0 = *reinterpret_cast<const f4*>(g + c * 8), g1 = *reinterpret_cast<const f4*>(g + c * 8 + 4);
+  const f4 b0 = *reinterpret_cast<const f4*>(b + c * 8), b1 = *reinterpret_cast<const f4*>(b + c * 8 + 4);
+  h8 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = (h16)((v[j] - mean) * rstd * g0[j] + b0[j]);
+    o[j + 4] = (h16)((v[j + 4] - mean) * rstd * g1[j] + b1[j]);
+  }
+  if (ok) stg16(y + (long)row * C + c * 8, __builtin_bit_cast(uint4, o));
+}
+
 // GroupNorm: one block per (frame, group).  Pass 1: mean; pass 2: centred second moment;
 // pass 3: normalise + affine.  Slab = S rows x cg contiguous channels at row stride C.
 // Loads are VW halfs wide (VW = 8/4/2 chosen from cg).
@@ -239,8 +277,23 @@ extern "C" int vda_layernorm(const void* x, int64_t ldx, void* y, const float* g
   VDA_CHECK_ARG(rows > 0 && C > 0 && C % 8 == 0 && C <= 2048, "C must be a multiple of 8, <= 2048");
   VDA_CHECK_ARG(ldx % 8 == 0 && ldx >= C, "ldx must be a multiple of 8 and >= C");
   VDA_CHECK_ARG(skip_period >= 0, "skip_period >= 0");
-  hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream,
-                     (const h16*)x, (long)ldx, (h16*)y, gamma, beta, rows, C, eps, skip_period);
+  hipStream_t st = (hipStream_t)stream;
+  if (C == 256 || C == 512 || C == 128) {
+    const int lpr = C / 8, rpb = 4 * (64 / lpr);  // rows per 256-thread block
+    const dim3 grid((rows + rpb - 1) / rpb);
+    if (lpr == 16)
+      hipLaunchKernelGGL(layernorm_narrow_kernel<16>, grid, dim3(256), 0, st, (const h16*)x, (long)ldx, (h16*)y, gamma,
+                         beta, rows, C, eps, skip_period);
+    else if (lpr == 32)
+      hipLaunchKernelGGL(layernorm_narrow_kernel<32>, grid, dim3(256), 0, st, (const h16*)x, (long)ldx, (h16*)y, gamma,
+                         beta, rows, C, eps, skip_period);
+    else
+      hipLaunchKernelGGL(layernorm_narrow_kernel<64>, grid, dim3(256), 0, st, (const h16*)x, (long)ldx, (h16*)y, gamma,
+                         beta, rows, C, eps, skip_period);
+  } else {
+    hipLaunchKernelGGL(layernorm_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, (const h16*)x, (long)ldx, (h16*)y,
+                       gamma, beta, rows, C, eps, skip_period);
+  }
   VDA_LAUNCH_CHECK();
   return 0;
 }
