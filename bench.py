@@ -13,7 +13,8 @@ Extra fields:
   roofline      dominant kernel = encoder MLP fc1 GEMM + GELU (vda gemm_kernel<..., GELU>), timed
                 per launch with HIP events on its launch stream inside the timed region;
                 achieved = algorithmic FLOPs per launch / mean launch time vs 2.5 PFLOP/s dense
-                fp16; traffic from profiles/<round>_pmc_fc1.json (rocprofv3 PMC, gfx950-corrected)
+                fp16; traffic from profiles/<round>_pmc_fc1.json (rocprofv3 PMC, gfx950-corrected),
+                mfma_busy_pmc from profiles/<round>_pmc_mfma.json (SQ_VALU_MFMA_BUSY_CYCLES pass)
   cpu_baseline  the oracle's fp32 PyTorch-CPU forward (oracle/vda_oracle.py), rank 0 / N=1 only,
                 on a bounded sample (a 4-frame ViT-L 518x518 clip) - a reported baseline only.
 """
@@ -146,8 +147,17 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        # MFMA-busy fraction of the same kernel class from the committed PMC pass
+        # (profiles/<round>_pmc_mfma.json: SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * CUs * 4))
+        mfma_busy = None
+        pmm = os.path.join(REPO, "profiles", "r01_pmc_mfma.json")
+        if os.path.exists(pmm):
+            with open(pmm) as f:
+                for name, e in json.load(f).get("kernels", {}).items():
+                    if "gemm256_kernel<2, 2, false, 1, false>" in name:
+                        mfma_busy = e.get("mfma_busy")
         roof = {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic,
+                "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": traffic, "mfma_busy_pmc": mfma_busy,
                 "kernel": f"gemm256_kernel<2,2,dense,GELU> (encoder fc1) M={M} N={4 * C} K={C}",
                 "flop_per_launch": flop, "avg_launch_ms": round(ms, 4), "launches": len(launches["enc_fc1"])}
 

@@ -409,17 +409,20 @@ __device__ __forceinline__ void rope_frag(h8& q, h8& k, int t, int c0, int C, fl
   }
 }
 
+#ifndef VDA_TA_NW
+#define VDA_TA_NW 4  // waves (heads of one site) per temporal-attention block
+#endif
 template <int DP>
-__global__ __launch_bounds__(256) void temporal_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+__global__ __launch_bounds__(64 * VDA_TA_NW) void temporal_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
                                                             int B, int T, int S, int H, int D, float scale_log2,
                                                             float rope_theta) {
   constexpr int NST = DP / 16;
   constexpr int NDT = (DP + 31) / 32;
   constexpr int DP32 = NDT * 32;
   constexpr int VSTR = DP32 + (DP32 > 32 ? 32 : 0);  // row stride (halfs) of the V tile
-  __shared__ __attribute__((aligned(16))) h16 sV[4][32 * VSTR];
+  __shared__ __attribute__((aligned(16))) h16 sV[VDA_TA_NW][32 * VSTR];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const long item = (long)blockIdx.x * 4 + wave;
+  const long item = (long)blockIdx.x * VDA_TA_NW + wave;
   const long nitems = (long)B * S * H;
   const bool active = item < nitems;
   const int hh = active ? (int)(item % H) : 0;
@@ -539,11 +542,11 @@ extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int
   VDA_CHECK_ARG(T > 0 && T <= 32, "temporal attention needs 1 <= T <= 32 (PE table length)");
   VDA_CHECK_ARG(D > 0 && D % 8 == 0 && D <= 128, "head dim must be a multiple of 8, <= 128");
   const long items = (long)B * S * H;
-  dim3 grid((unsigned)((items + 3) / 4));
+  dim3 grid((unsigned)((items + VDA_TA_NW - 1) / VDA_TA_NW));
   hipStream_t st = (hipStream_t)stream;
   const float sl = scale * 1.4426950408889634f;
   const int dp = (D + 15) / 16 * 16;
-#define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl, rope_theta)
+#define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(64 * VDA_TA_NW), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl, rope_theta)
   switch (dp) {
     case 16: VDA_TA(16); break;
     case 32: VDA_TA(32); break;
