@@ -958,10 +958,6 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         }
       }
     };
-    if (e.gamma) phase1(std::true_type{});
-    else phase1(std::false_type{});
-    __syncthreads();
-    TS(4);
     const int nout = (ACT == VDA_ACT_GEGLU) ? (p.N >> 1) : p.N;
     const int cout0 = (ACT == VDA_ACT_GEGLU) ? (n0 >> 1) : n0;
     // Phase 2: thread -> fixed (row0 + RPI * it, 16-byte chunk q).  Every iteration reuses the same
@@ -988,6 +984,26 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     const h16* r1p = (const h16*)(e.res ? e.res : e.res2);
     const long r1ld = e.res ? e.ldres : e.ldres2;
     const int nres = (e.res ? 1 : 0) + (e.res2 ? 1 : 0);
+    // A single residual (the encoder's proj / fc2 x += ..., the fusion adds) is requested in full
+    // here, before phase 1, so its 16 loads per thread overlap the activation / LDS staging instead
+    // of stalling phase 2 four times per tile (in situ, proj ran 45 % over its residual-free time).
+    // The residual may alias the output: this tile is written only by this block, in phase 2.
+    constexpr bool RPF = XR == 2 && ACT == VDA_ACT_NONE && !CONV && !ROWB;  // NIT = 16 chunks = 64 VGPRs; the
+    // other instantiations have no register room for it (GELU / GEGLU / conv / row bias: spills)
+    h8 rpre[RPF ? NIT : 1];
+    if constexpr (RPF) {
+      if (nres == 1) {
+        const __amdgpu_buffer_rsrc_t rr = rsrc(r1p, r1ld);
+        const unsigned vr = voff(r1ld), sr = (unsigned)(RPI * r1ld * 2);
+#pragma unroll
+        for (int it = 0; it < NIT; ++it)
+          rpre[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, vr + it * sr, 0, 0));
+      }
+    }
+    if (e.gamma) phase1(std::true_type{});
+    else phase1(std::false_type{});
+    __syncthreads();
+    TS(4);
     auto phase2 = [&](auto nres_tag) {
       constexpr int NR = decltype(nres_tag)::value;
       __amdgpu_buffer_rsrc_t rr1, rr2;
@@ -1004,9 +1020,23 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
       }
     };
-    if (nres == 0) phase2(std::integral_constant<int, 0>{});
-    else if (nres == 1) phase2(std::integral_constant<int, 1>{});
-    else phase2(std::integral_constant<int, 2>{});
+    if (nres == 0) {
+      phase2(std::integral_constant<int, 0>{});
+    } else if (nres == 1) {
+      if constexpr (RPF) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+          const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
+          const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
+          const h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y)) + rpre[it];
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
+        }
+      } else {
+        phase2(std::integral_constant<int, 1>{});
+      }
+    } else {
+      phase2(std::integral_constant<int, 2>{});
+    }
     TS(5);
 #ifdef VDA_TS
     wait_vmcnt<0>();
