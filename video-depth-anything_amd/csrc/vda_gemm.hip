@@ -1010,13 +1010,30 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       unsigned vr1 = 0, sr1 = 0, vr2 = 0, sr2 = 0;
       if constexpr (NR >= 1) { rr1 = rsrc(r1p, r1ld); vr1 = voff(r1ld); sr1 = (unsigned)(RPI * r1ld * 2); }
       if constexpr (NR >= 2) { rr2 = rsrc((const h16*)e.res2, e.ldres2); vr2 = voff(e.ldres2); sr2 = (unsigned)(RPI * e.ldres2 * 2); }
-#pragma unroll 4
+      // residual loads run PD iterations ahead of their use (a rolling window instead of batches of
+      // 4 loads whose latency each batch waits out)
+      constexpr int PD = 4;
+      h8 q1[PD], q2[PD];
+      auto ld1 = [&](int it) { return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, vr1 + it * sr1, 0, 0)); };
+      auto ld2 = [&](int it) { return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, vr2 + it * sr2, 0, 0)); };
+#pragma unroll
+      for (int it = 0; it < PD && it < NIT; ++it) {
+        if constexpr (NR >= 1) q1[it] = ld1(it);
+        if constexpr (NR >= 2) q2[it] = ld2(it);
+      }
+#pragma unroll
       for (int it = 0; it < NIT; ++it) {
         const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
         const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
         h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-        if constexpr (NR >= 1) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, vr1 + it * sr1, 0, 0));
-        if constexpr (NR >= 2) t += __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, vr2 + it * sr2, 0, 0));
+        if constexpr (NR >= 1) {
+          t += q1[it % PD];
+          if (it + PD < NIT) q1[it % PD] = ld1(it + PD);
+        }
+        if constexpr (NR >= 2) {
+          t += q2[it % PD];
+          if (it + PD < NIT) q2[it % PD] = ld2(it + PD);
+        }
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
       }
     };
