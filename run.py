@@ -49,6 +49,8 @@ def parse(argv=None):
     p.add_argument("--vis_format", type=str, default="y4m", choices=["y4m", "gif", "png", "webp", "mp4"])
     p.add_argument("--checkpoint", type=str, default=None)
     p.add_argument("--synthetic_weights", action="store_true")
+    p.add_argument("--windows_per_batch", type=int, default=1,
+                   help="windows per forward in the long-video path (2: ~3%% more frames/s on MI355X)")
     a = p.parse_args(argv)
     assert a.inference_length > len(a.keyframe_list) + 2, "Inference length to small for the number of geiven keyframes"
     return a
@@ -79,7 +81,8 @@ def main(argv=None):
                                                 skip_tmp_block=args.skip_tmp_block)
     else:
         depths, fps = model.infer_video_depth(frames, target_fps, input_size=args.input_size, device=dev, fp32=args.fp32,
-                                              skip_tmp_block=args.skip_tmp_block and not args.original)
+                                              skip_tmp_block=args.skip_tmp_block and not args.original,
+                                              windows_per_batch=max(1, args.windows_per_batch))
     dur = time.time() - t0
     os.makedirs(args.output_dir, exist_ok=True)
     stem = os.path.splitext(os.path.basename(args.input_video))[0]
