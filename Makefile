@@ -8,7 +8,7 @@ SRCS    := $(wildcard $(PKG)/csrc/*.hip)
 OBJS    := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(SRCS))
 CXXFLAGS := --offload-arch=$(ARCH) -O3 -fPIC -std=c++17 -Wall -Wno-unused-result -I include -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form
 
-all: $(PKG)/libvda.so
+all: $(PKG)/libvda.so $(PKG)/libvda_torch.so
 
 # attention: no NaN inputs by construction, so max chains need no IEEE quieting (v_max3 straight
 # off the MFMA results instead of canonicalising v_max per score)
@@ -23,10 +23,26 @@ build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h $(PKG)/csrc/phi_table.h in
 $(PKG)/libvda.so: $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
 
+# torch.ops.vda.* (TORCH_LIBRARY registration over the C ABI): host-only C++ against the installed
+# PyTorch-ROCm headers, linked to libvda.so (found next to it through $$ORIGIN)
+TORCH_DIR := $(shell python3 -c "import os, torch; print(os.path.dirname(torch.__file__))" 2>/dev/null)
+TORCH_ABI := $(shell python3 -c "import torch; print(int(torch.compiled_with_cxx11_abi()))" 2>/dev/null)
+TORCH_CXXFLAGS := -std=c++17 -O2 -fPIC -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -D_GLIBCXX_USE_CXX11_ABI=$(TORCH_ABI) \
+	-I include -I $(TORCH_DIR)/include -I $(TORCH_DIR)/include/torch/csrc/api/include -I /opt/rocm/include
+TORCH_LDFLAGS := -shared -L $(TORCH_DIR)/lib -lc10 -lc10_hip -ltorch_cpu -ltorch_hip -ltorch \
+	-L $(PKG) -lvda -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,$(TORCH_DIR)/lib
+
+build/vda_torch.o: $(PKG)/csrc/vda_torch.cpp include/vda.h
+	@mkdir -p build
+	$(CXX) $(TORCH_CXXFLAGS) -c $< -o $@
+
+$(PKG)/libvda_torch.so: build/vda_torch.o $(PKG)/libvda.so
+	$(CXX) build/vda_torch.o -o $@ $(TORCH_LDFLAGS)
+
 tools/mfma_probe: tools/mfma_probe.hip
 	$(HIPCC) --offload-arch=$(ARCH) -O2 -Wno-unused-result $< -o $@
 
 clean:
-	rm -rf build $(PKG)/libvda.so
+	rm -rf build $(PKG)/libvda.so $(PKG)/libvda_torch.so
 
 .PHONY: all clean

@@ -88,10 +88,18 @@ int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int64_t ldy,
  * If `up_h`/`up_w` > 0, X is read through a bilinear align_corners=True upsample from
  * [BT, H, W, Cin] to [BT, up_h, up_w, Cin] (blocks.py:156-158 / dpt_temporal.py:92-94), and the
  * conv runs on the upsampled grid.
+ * `ws` / `ws_bytes`: a device workspace of vda_conv2d_workspace(...) bytes lets the strip-tiled
+ * 3x3 kernel split small maps' input channels over several work items (fp32 partial slices summed
+ * in a fixed order: deterministic).  NULL / 0 runs the same conv unsplit.  The library keeps no
+ * mutable device state of its own, so calls on different streams with their own workspaces may
+ * run concurrently.
  */
 int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
                int32_t Cin, int32_t Cout, int32_t ks, int32_t stride, int32_t pad,
-               int32_t pre_relu, int32_t up_h, int32_t up_w, const vda_epilogue* epi, void* stream);
+               int32_t pre_relu, int32_t up_h, int32_t up_w, const vda_epilogue* epi,
+               void* ws, int64_t ws_bytes, void* stream);
+int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
+                             int32_t stride, int32_t pad);
 
 /*
  * Row LayerNorm, fp32 statistics.  X rows of C halfs (row stride ldx); Y [rows, C] half.
@@ -156,8 +164,10 @@ int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W
 /*
  * Depth head tail (dpt_temporal.py:92-99, dpt.py:118-124, video_depth.py:63-64):
  * X [BT, Hin, Win, C] half (the output_conv1 result) is bilinearly resized (align_corners=True,
- * fp16 storage like the reference's autocast interpolate) into the caller's workspace
- * ws [BT, Ho, Wo, C] half, then conv3x3(C -> 32, +b1) -> ReLU -> conv1x1(32 -> 1, w2, +b2) -> ReLU.
+ * fp16 storage like the reference's autocast interpolate), then conv3x3(C -> 32, +b1) -> ReLU ->
+ * conv1x1(32 -> 1, w2, +b2) -> ReLU.  The resize is normally fused into the conv's patch staging
+ * (the resized map is never written); shapes that need it materialised use the caller's workspace
+ * ws [BT, Ho, Wo, C] half of vda_depth_head_workspace(...) bytes (0 = not needed: ws may be NULL).
  * The 3x3 conv keeps fp32 weights as an exact fp16 hi/lo split: w1 is half [64, 3, 3, C] with
  * rows 0..31 = fp16(w) and rows 32..63 = fp16(w - fp16(w)); both halves accumulate in fp32.
  * depth [BT, Ho, Wo] float.  C % 8 == 0.
@@ -165,6 +175,7 @@ int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W
 int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2,
                    const float* b2, float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win,
                    int32_t C, int32_t Ho, int32_t Wo, void* stream);
+int64_t vda_depth_head_workspace(int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo);
 
 /*
  * Frame preprocessing on the device: uint8 RGB frames [N, h, w, 3] (HWC) -> float [N, 3, H, W]

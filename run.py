@@ -74,7 +74,7 @@ def main(argv=None):
     frames, target_fps = VIO.read_video_frames(args.input_video, args.max_len, args.target_fps, args.max_res)
     total = len(frames)
     t0 = time.time()
-    if args.process_single_image and not args.original:
+    if args.process_single_image:  # checked before --original, as in the reference (run.py:93-100)
         depths, fps = model.infere_single_image(frames, target_fps, device=dev, fp32=args.fp32, input_size=args.input_size,
                                                 inference_length=args.inference_length, keyframe_list=args.keyframe_list,
                                                 align_each_new_frame=args.align_each_new_frame, warmup=True,

@@ -62,7 +62,7 @@ def test_conv_and_attention_validation():
     lib = _lib.lib()
     fake = ctypes.c_void_p(0x1000)
     e = _lib.Epilogue()
-    assert lib.vda_conv2d(fake, fake, fake, 1, 8, 8, 12, 16, 3, 1, 1, 0, 0, 0, e, None) == -22  # Cin % 8
+    assert lib.vda_conv2d(fake, fake, fake, 1, 8, 8, 12, 16, 3, 1, 1, 0, 0, 0, e, None, 0, None) == -22  # Cin % 8
     assert lib.vda_spatial_attention(fake, fake, 1, 10, 2, 32, 0.1, None) == -22                # D != 64
     assert lib.vda_temporal_attention(fake, fake, 1, 33, 4, 8, 16, 0.1, 0.0, None) == -22     # T > 32
     assert b"T <= 32" in lib.vda_last_error()
@@ -91,6 +91,27 @@ def test_torch_ops_registered_meta_shapes_and_no_cpu_kernel():
     assert torch.ops.vda.layernorm(x, x.new_empty(64, dtype=torch.float32), x.new_empty(64, dtype=torch.float32),
                                    1e-6, 9).shape == (90, 64)
     img = torch.empty(2, 3, 28, 42, device="meta")
-    assert torch.ops.vda.patch_im2col(img, 640, False).shape == (2 * 7, 640)
+    assert torch.ops.vda.patch_im2col(img, 640, torch.float16).shape == (2 * 7, 640)
+    assert torch.ops.vda.patch_im2col(img, 588, torch.float32).dtype == torch.float32
+    assert torch.ops.vda.temporal_attention(torch.empty(2 * 32 * 5, 3 * 256, device="meta", dtype=torch.float16),
+                                            2, 32, 5, 8, 32, rope_theta=1e4).shape == (2 * 32 * 5, 256)
+    up = torch.ops.vda.conv2d(m, wc[:, :, :, :64], 3, 1, 1, None, False, 0, None, None, [20, 24])
+    assert up.shape == (2, 20, 24, 32)
+    o = torch.empty(100, 96, device="meta", dtype=torch.float16)
+    assert torch.ops.vda.gemm.out(x, w, act=0, out=o) is not None
     with pytest.raises(NotImplementedError):
         torch.ops.vda.upsample_bilinear(torch.zeros(1, 2, 2, 8, dtype=torch.float16), 4, 4)
+
+
+def test_workspace_queries():
+    """Workspaces are the caller's (no library-global device buffers): the strip conv's split
+    workspace is sized by vda_conv2d_workspace, the depth head's resize workspace by
+    vda_depth_head_workspace (0 when the fused kernel serves the shape)."""
+    lib = _lib.lib()
+    # ViT-L layer4_rn at 19^2 (32 frames, Cin 1024 -> 256): split into fp32 slices of M x 256
+    n = lib.vda_conv2d_workspace(32, 19, 19, 1024, 256, 3, 1, 1)
+    assert n > 0 and n % (32 * 19 * 19 * 256 * 4) == 0
+    assert lib.vda_conv2d_workspace(32, 148, 148, 256, 256, 3, 1, 1) == 0   # implicit GEMM: no workspace
+    assert lib.vda_conv2d_workspace(32, 37, 37, 1024, 256, 3, 2, 1) == 0    # stride 2: no workspace
+    assert lib.vda_depth_head_workspace(32, 296, 296, 128, 518, 518) == 0   # fused resize: none
+    assert lib.vda_depth_head_workspace(2, 20, 20, 32, 518, 518) == 2 * 518 * 518 * 32 * 2  # C % 64: materialised

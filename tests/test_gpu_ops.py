@@ -279,15 +279,57 @@ def test_ops_reject_cpu_tensors():
         ops.gemm(torch.zeros(4, 8, dtype=torch.float16), torch.zeros(4, 8, dtype=torch.float16))
 
 
-def test_torch_ops_dispatch_to_libvda():
-    """torch.ops.vda.* (CUDA key) run the same kernels as ops.* (bitwise)."""
+def test_c_abi_direct_matches_torch_ops():
+    """The C ABI called straight through ctypes (as a non-torch host would) == torch.ops.vda.* (the native
+    TORCH_LIBRARY registration over the same entry points), bitwise."""
+    import ctypes
+    from vda_amd import _lib
     import vda_amd.torch_ops  # noqa: F401
+    lib = _lib.lib()
+    st = torch.cuda.current_stream().cuda_stream
     x, w, b = rnd(300, 128, seed=70), rnd(256, 128, scale=128 ** -0.5, seed=71), rnd(256, scale=0.1, seed=72)
-    y0 = ops.gemm(h(x), h(w), bias=f32(b), act=ACT_GELU)
-    y1 = torch.ops.vda.gemm(h(x), h(w), f32(b), None, 1, 1, None, None, None, ACT_GELU)
-    assert torch.equal(y0, y1)
+    xh, wh, bf = h(x), h(w), f32(b)
+    y = torch.empty(300, 256, dtype=torch.float16, device=DEV)
+    e = _lib.Epilogue()
+    e.bias, e.rdiv, e.rmod, e.act = bf.data_ptr(), 1, 1, ACT_GELU
+    assert lib.vda_gemm(xh.data_ptr(), 128, wh.data_ptr(), y.data_ptr(), 256, 300, 256, 128, ctypes.byref(e), st) == 0
+    y1 = torch.ops.vda.gemm(xh, wh, bf, None, 1, 1, None, None, None, ACT_GELU)
+    assert torch.equal(y, y1) and torch.equal(y, ops.gemm(xh, wh, bias=bf, act=ACT_GELU))
     m = h(rnd(2, 9, 11, 64, seed=73))
     assert torch.equal(torch.ops.vda.upsample_bilinear(m, 17, 21), ops.upsample_bilinear(m, 17, 21))
+    # strip conv at 19^2 with Cin 1024 (layer4_rn): the caller's split workspace (C ABI) vs the op, which
+    # allocates the same workspace per call from the caching allocator; and the unsplit (ws = NULL) run
+    xc = h(rnd(4, 19, 19, 1024, seed=74))
+    wc = h(rnd(256, 3, 3, 1024, scale=(9 * 1024) ** -0.5, seed=75))
+    nws = lib.vda_conv2d_workspace(4, 19, 19, 1024, 256, 3, 1, 1)
+    assert nws > 0
+    ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+    yc = torch.empty(4, 19, 19, 256, dtype=torch.float16, device=DEV)
+    yn = torch.empty_like(yc)
+    e0 = _lib.Epilogue()
+    e0.rdiv = e0.rmod = 1
+    args = (4, 19, 19, 1024, 256, 3, 1, 1, 0, 0, 0, ctypes.byref(e0))
+    assert lib.vda_conv2d(xc.data_ptr(), wc.data_ptr(), yc.data_ptr(), *args, ws.data_ptr(), nws, st) == 0
+    assert lib.vda_conv2d(xc.data_ptr(), wc.data_ptr(), yn.data_ptr(), *args, None, 0, st) == 0
+    assert torch.equal(yc, ops.conv2d(xc, wc))
+    ref = F.conv2d(xc.float().permute(0, 3, 1, 2), wc.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    assert rel(yc, ref) < 2e-3 and rel(yn, ref) < 2e-3
+
+
+def test_depth_head_allocates_no_resize_workspace():
+    """The fused depth head never materialises the 518^2 resized map: the op's peak memory is its output
+    plus the inputs (ops.depth_head used to reserve [BT, 518, 518, 128] fp16 per call)."""
+    x = h(rnd(2, 296, 296, 128, scale=0.5, seed=76))
+    w1 = h(rnd(64, 3, 3, 128, scale=0.03, seed=77))
+    b1, w2, b2 = f32(rnd(32, seed=78)), f32(rnd(32, seed=79)), f32(rnd(1, seed=80))
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    torch.cuda.reset_peak_memory_stats()
+    d = ops.depth_head(x, w1, b1, w2, b2, 518, 518)
+    torch.cuda.synchronize()
+    extra = torch.cuda.max_memory_allocated() - base
+    assert d.shape == (2, 518, 518)
+    assert extra <= 2 * 518 * 518 * 4 + (4 << 20), extra  # the fp32 depth (+ allocator rounding)
 
 
 @pytest.mark.parametrize("Cin,H,W,relu", [(256, 130, 140, False), (128, 129, 131, True)])

@@ -149,3 +149,41 @@ def test_depth_resize_kernel_vs_torch(src, dst):
     # ~1e-5, i.e. ~1e-5 of the local depth step: bound it relative to the depth range
     assert (out - ref).abs().max().item() <= 1e-4 * d.abs().max().item()
     assert vda_oracle.rel_l1(out, ref) <= 2e-5  # white-noise depth: the worst case for weight rounding
+
+
+def test_config1_vits_8x518_video_cpu_plumbing():
+    """BASELINE configs[0]: an 8-frame 518x518 video through the long-video driver with the fp32 CPU
+    oracle as the clip forward.  The reference pads the 8 frames to one 32-frame window with copies of
+    the last frame (video_depth.py:351-354) and returns the first 8; the driver must reproduce exactly
+    that plumbing: equal to one oracle forward of the padded clip, cut to 8 frames."""
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    g = np.random.default_rng(11)
+    frames = g.integers(0, 256, (8, 518, 518, 3), dtype=np.uint8)
+    sd = recipe_state_dict("vits")
+    depth, fps = V.infer_video_depth(_oracle_forward(sd), frames, 30, input_size=518, device="cpu",
+                                     io=vda_oracle.TorchIO)
+    assert depth.shape == (8, 518, 518) and fps == 30
+    idx = V.window_frame_indices(0, 8)
+    assert idx == list(range(8)) + [7] * 24
+    x = vda_oracle.TorchIO.preprocess(torch.from_numpy(frames[idx]), (518, 518)).unsqueeze(0)
+    ref = vda_oracle.forward(sd, "vits", x)[0, :8].numpy()
+    err = float(np.abs(depth - ref).sum() / np.abs(ref).sum())
+    assert err <= 1e-6, err
+
+
+@pytest.mark.gpu
+def test_video_device_memory_flat_in_video_length():
+    """Each window's depth leaves the device right after its resize: the peak device
+    memory of a 4x longer video stays the same."""
+    def fwd(x):
+        return x[:, :, 0].contiguous()
+    peaks = []
+    for n in (60, 240):
+        frames = np.random.default_rng(n).integers(0, 256, (n, 48, 64, 3), dtype=np.uint8)
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        d, _ = V.infer_video_depth(fwd, frames, 24, input_size=56, device="cuda")
+        assert d.shape == (n, 48, 64)
+        peaks.append(torch.cuda.max_memory_allocated() - base)
+    assert peaks[1] <= peaks[0] * 1.1 + (1 << 20), peaks

@@ -104,3 +104,44 @@ def test_cli_end_to_end(tmp_path, single):
         ref, _ = m.infer_video_depth(frames, fps, input_size=56)
     assert d.shape == ref.shape == ((39 if single else 40), 42, 56)
     assert np.abs(d - ref).max() <= 1e-6 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.gpu
+def test_cli_on_reference_golden_video(tmp_path):
+    """run.py end to end vs the REFERENCE's own infer_video_depth output (tests/golden/video_vits_57f.npz,
+    made by tests/golden/make_golden.py): the golden's frames as a .npz frame stack -> run.py -> npz."""
+    import sys
+    sys.path.insert(0, REPO)
+    import json
+    import run as cli
+    z = np.load(os.path.join(REPO, "tests", "golden", "video_vits_57f.npz"), allow_pickle=False)
+    meta = json.loads(str(z["meta"]))
+    p = str(tmp_path / "golden.npz")
+    np.savez(p, frames=z["frames"], fps=np.float64(meta["fps"]))
+    out = tmp_path / "out"
+    d = cli.main(["--input_video", p, "--output_dir", str(out), "--encoder", meta["encoder"], "--input_size",
+                  str(meta["input_size"]), "--synthetic_weights", "--save_npz"])
+    npz = np.load(str(out / "VideoDepthAny_vits_golden_depths.npz"))["depths"]
+    assert np.array_equal(npz, d) and d.shape == z["depth"].shape
+    err = float(np.abs(d - z["depth"]).sum() / np.abs(z["depth"]).sum())
+    print(f"run.py on the reference golden video: rel-L1 = {err:.3e}")
+    assert err <= 1e-3
+
+
+@pytest.mark.gpu
+def test_cli_single_image_wins_over_original(tmp_path):
+    """--process_single_image is checked before --original (reference run.py:93-100): the streaming
+    driver runs and the outputs are named Single_*."""
+    import sys
+    sys.path.insert(0, REPO)
+    import run as cli
+    fr = _frames(n=36, h=42, w=56)
+    p = str(tmp_path / "clip.y4m")
+    VIO.write_y4m(p, fr, 24)
+    base = ["--input_video", p, "--encoder", "vits", "--input_size", "56", "--synthetic_weights", "--save_npz",
+            "--process_single_image", "--keyframe_list", "2", "12", "--align_each_new_frame"]
+    d1 = cli.main(base + ["--output_dir", str(tmp_path / "a")])
+    d2 = cli.main(base + ["--output_dir", str(tmp_path / "b"), "--original"])
+    assert d1.shape == d2.shape == (35, 42, 56)  # the streaming driver's frame count
+    assert np.array_equal(d1, d2)
+    assert os.path.exists(str(tmp_path / "b" / "Single_VideoDepthAny_vits_clip_depths.npz"))

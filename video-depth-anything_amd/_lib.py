@@ -12,12 +12,14 @@ from ctypes import c_float, c_int32, c_int64, c_void_p, POINTER
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so")  # override: tuning experiments only
+TORCH_LIB_PATH = os.path.join(_HERE, "libvda_torch.so")  # TORCH_LIBRARY(vda) over the C ABI (csrc/vda_torch.cpp)
 
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
-    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_layernorm", "vda_groupnorm", "vda_groupnorm_workspace",
+    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
+    "vda_groupnorm", "vda_groupnorm_workspace",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
-    "vda_depth_head", "vda_preprocess_frames", "vda_depth_resize",
+    "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
     "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_strip_split",
@@ -56,7 +58,8 @@ def _declare(lib):
         "vda_version": ([], ctypes.c_char_p),
         "vda_last_error": ([], ctypes.c_char_p),
         "vda_gemm": ([P, L, P, P, L, I, I, I, EP, P], I),
-        "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P], I),
+        "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P, L, P], I),
+        "vda_conv2d_workspace": ([I, I, I, I, I, I, I, I], L),
         "vda_layernorm": ([P, L, P, P, P, I, I, F, I, P], I),
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
         "vda_groupnorm_workspace": ([I, I, I, I], L),
@@ -65,6 +68,7 @@ def _declare(lib):
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),
         "vda_patch_im2col": ([P, P, I, I, I, I, P], I),
         "vda_depth_head": ([P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
+        "vda_depth_head_workspace": ([I, I, I, I, I, I], L),
         "vda_preprocess_frames": ([P, P, I, I, I, I, I, POINTER(F), POINTER(F), P], I),
         "vda_depth_resize": ([P, P, I, I, I, I, I, P], I),
         "vda_gemm_f32": ([P, L, P, P, L, I, I, I, EP, P], I),
@@ -110,6 +114,28 @@ def lib():
         raise VDAUnavailable(_load_error) from e
     _lib = l
     return _lib
+
+
+_torch_ops = None
+
+
+def torch_ops():
+    """``torch.ops.vda`` after loading libvda_torch.so (raises VDAUnavailable if it cannot be loaded).
+    libvda.so is loaded first through ctypes from the same path, so the tuning hooks set through
+    ``lib()`` act on the library the operators call."""
+    global _torch_ops
+    if _torch_ops is not None:
+        return _torch_ops
+    lib()
+    if not os.path.exists(TORCH_LIB_PATH):
+        raise VDAUnavailable(f"libvda_torch.so not found at {TORCH_LIB_PATH}; run `make` (or __graft_entry__.build())")
+    import torch
+    try:
+        torch.ops.load_library(TORCH_LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the runtime
+        raise VDAUnavailable(f"failed to load {TORCH_LIB_PATH}: {e}") from e
+    _torch_ops = torch.ops.vda
+    return _torch_ops
 
 
 def check(rc: int, what: str):

@@ -374,12 +374,16 @@ int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* 
 // Depth tail straight from the UN-resized output_conv1 map x [BT, Hs, Ws, C] (C % 64 == 0, Hs <= H,
 // Ws <= W): the bilinear resize is computed while the halo patch is built (UPS), so the resized map
 // (2.2 GB at ViT-L 32x518^2) is never written.  Returns 1 when the shape is not served.
-int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
-                         float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st) {
-  if (C % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return 1;
+bool vda_depth_halo_fused_serves(int Hs, int Ws, int H, int W, int C) {
+  if (C % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return false;
   // the staged source region of a tile (<= floor(17 * scale) + 2 rows / columns) must fit 192 pixels
   const float sy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f, sx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
-  if (((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) > 192) return 1;
+  return ((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) <= 192;
+}
+
+int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
+                         float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st) {
+  if (!vda_depth_halo_fused_serves(Hs, Ws, H, W, C)) return 1;
   if (g_num_cus == 0) {
     int dev = 0, n = 0;
     (void)hipGetDevice(&dev);

@@ -40,7 +40,11 @@ extern "C" int vda_debug_timestamps(void* host) {
 int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
                    int BT, int H, int W, int C, hipStream_t st);
 int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
-                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st);
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, void* ws,
+                   long ws_bytes, hipStream_t st);
+bool vda_conv_strip_serves(int W, int Cin, int Cout);
+long vda_conv_strip_ws_bytes(int BT, int H, int W, int Cin, int Cout);
+bool vda_depth_halo_fused_serves(int Hs, int Ws, int H, int W, int C);
 int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
                   int Cout, hipStream_t st);
 int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
@@ -1276,10 +1280,28 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   return launch<false>(p, (hipStream_t)stream);
 }
 
+// The strip-tiled 3x3 conv (vda_strip.hip) serves 3x3 / s1 / p1 convs with 256 output channels and
+// Cin >= 512 on maps up to 160 wide (layer2..4_rn; measured 10-14% faster there, 1-4% slower than the
+// implicit GEMM at Cin = 256), and any Cout = 256 3x3 conv whose 256-pixel strip tiles would fill at
+// most half the CUs (19^2 maps: the strip kernel then splits the input channels over several work
+// items).  vda_debug_force_tile(-3) routes every Cout = 256 conv to it, (-2) none.
+static bool conv_takes_strip(int BT, int H, int W, int Cin, int Cout, int ks, int stride, int pad, int up_h) {
+  if (up_h > 0 || ks != 3 || stride != 1 || pad != 1 || !vda_conv_strip_serves(W, Cin, Cout)) return false;
+  const long strip_tiles = (long)BT * ((H * W + 255) / 256);
+  return g_force_tile == -3 || (g_force_tile == -1 && (Cin >= 512 || strip_tiles * 2 <= cu_count()));
+}
+
+extern "C" int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
+                                        int32_t stride, int32_t pad) {
+  if (BT <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  if (!conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0)) return 0;
+  return vda_conv_strip_ws_bytes(BT, H, W, Cin, Cout);
+}
+
 extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
                           int32_t Cin, int32_t Cout, int32_t ks, int32_t stride, int32_t pad,
                           int32_t pre_relu, int32_t up_h, int32_t up_w, const vda_epilogue* epi,
-                          void* stream) {
+                          void* ws, int64_t ws_bytes, void* stream) {
   VDA_CHECK_ARG(x && w && y, "null pointer");
   VDA_CHECK_ARG(BT > 0 && H > 0 && W > 0 && Cin > 0 && Cout > 0 && ks > 0 && stride > 0 && pad >= 0,
                 "bad conv geometry");
@@ -1312,17 +1334,10 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
     }
     return launch_reg_conv(p, (hipStream_t)stream);
   }
-  // 3x3 convs with 256 output channels and Cin >= 512 on maps up to 160 wide (layer2..4_rn): strip-tiled
-  // halo kernel (vda_strip.hip; measured 10-14% faster there, 1-4% slower than the implicit GEMM at
-  // Cin = 256); vda_debug_force_tile(-3) routes every Cout = 256 conv to it, (-2) none
-  // ... and any Cout = 256 3x3 conv whose 256-pixel strip tiles would fill at most half the CUs (19^2
-  // maps: the strip kernel then splits the input channels over several work items)
-  const long strip_tiles = (long)BT * ((H * W + 255) / 256);
-  const bool strip_ok = g_force_tile == -3 || (g_force_tile == -1 && (Cin >= 512 || strip_tiles * 2 <= cu_count()));
-  if (strip_ok && ks == 3 && stride == 1 && pad == 1 && Cout == 256 && !p.epi.gamma && !p.epi.rowbias &&
+  if (conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0) && !p.epi.gamma && !p.epi.rowbias &&
       (!p.epi.res || p.epi.ldres == Cout) && (!p.epi.res2 || p.epi.ldres2 == Cout)) {
     rc = vda_conv_strip(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, BT, H, W,
-                        Cin, Cout, (hipStream_t)stream);
+                        Cin, Cout, ws, ws ? ws_bytes : 0, (hipStream_t)stream);
     if (rc != 1) return rc;
   }
   // large 3x3 maps with 128 output channels (output_conv1 at 296^2): halo-tiled kernel (vda_depth.hip)
@@ -1338,7 +1353,7 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
 extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                               float* depth, void* ws, int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho,
                               int32_t Wo, void* stream) {
-  VDA_CHECK_ARG(x && w1 && b1 && w2 && b2 && depth && ws, "null pointer");
+  VDA_CHECK_ARG(x && w1 && b1 && w2 && b2 && depth, "null pointer");
   VDA_CHECK_ARG(BT > 0 && Hin > 0 && Win > 0 && Ho > 0 && Wo > 0, "bad depth-head geometry");
   VDA_CHECK_ARG(C % 8 == 0, "depth head needs C % 8 == 0");
   hipStream_t st = (hipStream_t)stream;
@@ -1349,6 +1364,7 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
     rc = vda_depth_halo_fused(x, w1, b1, w2, b2, depth, BT, Hin, Win, Ho, Wo, C, st);
     if (rc != 1) return rc;
   }
+  VDA_CHECK_ARG(ws, "depth head: this shape needs the resize workspace (vda_depth_head_workspace)");
   // 1) bilinear (align_corners=True) resize of the output_conv1 map to (Ho, Wo), fp16 like the
   //    reference's autocast interpolate (dpt_temporal.py:92-94)
   rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
@@ -1390,6 +1406,12 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   }
   VDA_LAUNCH_CHECK();
   return 0;
+}
+
+extern "C" int64_t vda_depth_head_workspace(int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo) {
+  if (BT <= 0 || Hin <= 0 || Win <= 0 || C <= 0 || Ho <= 0 || Wo <= 0) return 0;
+  if (g_force_tile < 9 && vda_depth_halo_fused_serves(Hin, Win, Ho, Wo, C)) return 0;  // fused: no resized map
+  return (int64_t)BT * Ho * Wo * C * 2;
 }
 
 extern "C" int vda_debug_force_tile(int32_t cfg) {

@@ -244,13 +244,39 @@ __global__ __launch_bounds__(256) void strip_finish_kernel(const float* __restri
 }
 
 int g_st_cus = 0;
-// Split workspace: a static device buffer (allocated with the code object, so no entry point
-// allocates device memory and split convs stay capturable in a hipGraph).  96 MiB covers ViT-L 32 x
-// 19^2 (and 19 x 33 at 518 x 924) in 4 splits; a split that would not fit is not chosen.  Library-
-// global: callers must not run split convs concurrently on two streams.
-constexpr long ST_WS_FLOATS = 24L << 20;
-__device__ float g_st_ws[ST_WS_FLOATS];
 int g_st_force_split = 0;  // tuning override (vda_debug_strip_split)
+
+int st_cus() {
+  if (g_st_cus == 0) {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    g_st_cus = n > 0 ? n : 256;
+  }
+  return g_st_cus;
+}
+
+// Split count for a served shape: minimise rounds x steps-per-item, charging a split its workspace
+// round trip (s slices written + read, ~4 TB/s) in units of a ~1.1 us pipeline step.  Only splits whose
+// fp32 slices fit `ws_floats` are considered (the caller's workspace; < 0 = unlimited, for the query).
+int st_split(int BT, int H, int W, int Cin, long ws_floats) {
+  const int nslab = Cin / ST_SLAB;
+  const long M = (long)BT * H * W;
+  const long nt = (long)BT * ((H * W + ST_M - 1) / ST_M);
+  auto fits = [&](int s) { return s == 1 || ws_floats < 0 || (long)s * M * ST_N <= ws_floats; };
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 8; s *= 2) {
+    if (nslab % s || !fits(s)) continue;
+    const long items = nt * s;
+    const double rounds = (double)((items + st_cus() - 1) / st_cus());
+    const double ws_us = s > 1 ? 2.0 * s * M * ST_N * 4 / 4e12 * 1e6 : 0.0;
+    const double cost = rounds * (nslab / s) * 9 + ws_us / 1.1;
+    if (cost < best_cost * 0.97) { best_cost = cost; best = s; }
+  }
+  if (g_st_force_split > 0 && nslab % g_st_force_split == 0 && fits(g_st_force_split)) best = g_st_force_split;
+  return best;
+}
 
 }  // namespace
 
@@ -259,17 +285,26 @@ extern "C" int vda_debug_strip_split(int32_t nsplit) {
   return 0;
 }
 
+bool vda_conv_strip_serves(int W, int Cin, int Cout) {
+  return Cout == ST_N && Cin % ST_SLAB == 0 && W <= ST_MAXW && W >= 16;
+}
+
+// Bytes of fp32 split workspace the strip conv would use for this shape (0: no split).
+long vda_conv_strip_ws_bytes(int BT, int H, int W, int Cin, int Cout) {
+  if (!vda_conv_strip_serves(W, Cin, Cout)) return 0;
+  const int s = st_split(BT, H, W, Cin, -1);
+  return s > 1 ? (long)s * BT * H * W * ST_N * 4 : 0;
+}
+
 // Serves 3x3 / s1 / p1 convs with Cout == 256, Cin % 32 == 0, 16 <= W <= 160 (caller checks the
 // epilogue: bias, ReLU, res / res2 with row stride Cout).  Returns 1 when the shape is not served.
+// `ws` / `ws_bytes`: the caller's fp32 split workspace (may be NULL / 0: no input-channel split).
+// Nothing library-global is written, so concurrent calls on different streams with their own
+// workspaces are safe.
 int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
-                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st) {
-  if (Cout != ST_N || Cin % ST_SLAB != 0 || W > ST_MAXW || W < 16) return 1;
-  if (g_st_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_st_cus = n > 0 ? n : 256;
-  }
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, void* ws_ptr,
+                   long ws_bytes, hipStream_t st) {
+  if (!vda_conv_strip_serves(W, Cin, Cout)) return 1;
   StripParams p{};
   p.x = (const h16*)x; p.w = (const h16*)w; p.y = (h16*)y; p.bias = bias;
   p.res = (const h16*)res; p.res2 = (const h16*)res2;
@@ -278,33 +313,18 @@ int vda_conv_strip(const void* x, const void* w, void* y, const float* bias, int
   const long nt = (long)BT * p.tiles_per_frame;
   if (nt > 0x7fffffffL / 8) return vda_set_error(-22, "conv: too many tiles");
   p.ntiles = (int)nt;
-  // split count: minimise rounds x steps-per-item, charging a split its workspace round trip
-  // (s slices written + read, ~4 TB/s) in units of a ~1.1 us pipeline step
   const int nslab = Cin / ST_SLAB;
   const long M = (long)BT * H * W;
-  int best = 1;
-  double best_cost = 1e30;
-  for (int s = 1; s <= 8; s *= 2) {
-    if (nslab % s || (s > 1 && (long)s * M * ST_N > ST_WS_FLOATS)) continue;
-    const long items = nt * s;
-    const double rounds = (double)((items + g_st_cus - 1) / g_st_cus);
-    const double ws_us = s > 1 ? 2.0 * s * M * ST_N * 4 / 4e12 * 1e6 : 0.0;
-    const double cost = rounds * (nslab / s) * 9 + ws_us / 1.1;
-    if (cost < best_cost * 0.97) { best_cost = cost; best = s; }
-  }
-  if (g_st_force_split > 0 && nslab % g_st_force_split == 0 && (long)g_st_force_split * M * ST_N <= ST_WS_FLOATS)
-    best = g_st_force_split;
+  const int best = st_split(BT, H, W, Cin, ws_ptr ? ws_bytes / 4 : 0);
   p.nsplit = best;
   p.nsl = nslab / best;
-  float* ws = nullptr;
+  float* ws = (float*)ws_ptr;
   if (best > 1) {
-    if (hipGetSymbolAddress((void**)&ws, HIP_SYMBOL(g_st_ws)) != hipSuccess || !ws)
-      return vda_set_error(-22, "conv: split workspace symbol unavailable");
     p.ws = ws;
     p.ws_slice = M * ST_N;
   }
   const long nitems = nt * best;
-  const int grid = (int)(nitems < g_st_cus ? nitems : g_st_cus);
+  const int grid = (int)(nitems < st_cus() ? nitems : st_cus());
   hipLaunchKernelGGL(strip_conv_kernel, dim3(grid), dim3(512), 0, st, p);
   if (best > 1) {
     const long n4 = M * ST_N / 4;

@@ -159,51 +159,112 @@ def stitch(depth_list: List[np.ndarray], n_frames: int) -> np.ndarray:
 
 
 # ---- driver ---------------------------------------------------------------------------------
+class _HostSink:
+    """Moves each window's resized depth [32, h, w] off the device as soon as it exists (as the
+    reference does, video_depth.py:372-373), so device memory stays flat in the video length.  On a
+    GPU the copies go through a ring of two pinned staging buffers with non-blocking D2H copies, so
+    the next window's forward is enqueued while the previous window drains."""
+
+    def __init__(self, device: torch.device):
+        self.gpu = device.type == "cuda"
+        self.ring: list = []
+        self.pending: list = []  # (window id, staging slot, event)
+        self.out = {}
+
+    def _drain(self, keep: int):
+        while len(self.pending) > keep:
+            k, slot, ev = self.pending.pop(0)
+            ev.synchronize()
+            self.out[k] = slot.numpy().copy()
+
+    def put(self, k: int, d: torch.Tensor):
+        if not self.gpu:
+            self.out[k] = d.detach().to("cpu", torch.float32).numpy().copy()
+            return
+        self._drain(1)  # slot (len(pending) % 2) is free after this
+        busy = {id(s) for _, s, _ in self.pending}
+        slot = next((s for s in self.ring if id(s) not in busy and s.shape == d.shape), None)
+        if slot is None:
+            slot = torch.empty(d.shape, dtype=torch.float32, pin_memory=True)
+            self.ring.append(slot)
+            self.ring = self.ring[-2:]
+        slot.copy_(d, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((k, slot, ev))
+
+    def result(self):
+        self._drain(0)
+        return self.out
+
+
+def _gather_round(buf: torch.Tensor, rank: int, world: int, group):
+    """Gather one round's per-rank window buffers [n, 32, h, w] to rank 0 (RCCL on GPU tensors; gloo
+    takes host copies).  Returns the list of world buffers on rank 0, None elsewhere."""
+    import torch.distributed as dist
+    cpu = dist.get_backend(group) == "gloo"
+    src = buf.cpu() if cpu else buf
+    bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
+    dist.gather(src, bufs, dst=0, group=group)
+    return bufs
+
+
 def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, target_fps, input_size: int = 518,
                       device="cuda", windows_per_batch: int = 1, rank: int = 0, world: int = 1, group=None,
                       io=DeviceIO):
     """Depth for every frame of ``frames`` (uint8 [N, h, w, 3] numpy or tensor).
 
     ``forward(x[B, 32, 3, H, W]) -> depth[B, 32, H, W]`` is the clip forward (the model, or any
-    callable).  With world > 1, window k runs on rank k % world and the per-window depth maps are
-    gathered to rank 0 over ``group`` (torch.distributed); rank 0 returns (depth, fps), others
-    return (None, fps).
+    callable).  With world > 1, window k runs on rank k % world: round r is windows
+    r*world .. r*world + world - 1, one per rank, and each round's (or each ``windows_per_batch``
+    rounds') depth maps are gathered to rank 0 as soon as they exist, so no rank ever holds more than
+    one batch of windows on the device.  Rank 0 keeps the windows in host memory and stitches;
+    rank 0 returns (depth, fps), others (None, fps).
     """
     if not isinstance(frames, torch.Tensor):
         frames = torch.from_numpy(np.ascontiguousarray(frames))
     n = frames.shape[0]
     h, w = int(frames.shape[1]), int(frames.shape[2])
     size = net_input_size(h, w, input_size)
-    starts = window_starts(n)
-    mine = [k for k in range(len(starts)) if k % world == rank]
+    nwin = len(window_starts(n))
+    rounds = (nwin + world - 1) // world
     dev = torch.device(device)
-    out = {}
-    for b0 in range(0, len(mine), windows_per_batch):
-        ks = mine[b0:b0 + windows_per_batch]
-        idx = [window_frame_indices(k, n) for k in ks]
-        uniq = sorted(set(i for row in idx for i in row))
-        pre = io.preprocess(frames[uniq].to(dev), size)
-        pos = {f: j for j, f in enumerate(uniq)}
-        x = torch.stack([pre[[pos[i] for i in row]] for row in idx], 0)
-        with torch.no_grad():
-            d = forward(x).float()  # [B, 32, H, W]
-        d = io.resize_depth(d.flatten(0, 1), (h, w)).view(len(ks), INFER_LEN, h, w)
-        for j, k in enumerate(ks):
-            out[k] = d[j]
-    if world > 1:
-        # gather every rank's windows to rank 0 (rank r owns windows r, r + world, ...)
-        import torch.distributed as dist
-        nwin = len(starts)
-        per = (nwin + world - 1) // world
-        mine_t = torch.zeros(per, INFER_LEN, h, w, dtype=torch.float32, device=dev)
-        for j, k in enumerate(mine):
-            mine_t[j] = out[k]
-        bufs = [torch.empty_like(mine_t) for _ in range(world)] if rank == 0 else None
-        dist.gather(mine_t, bufs, dst=0, group=group)
-        if rank != 0:
-            return None, target_fps
-        out = {k: bufs[k % world][k // world] for k in range(nwin)}
+    sink = _HostSink(dev) if rank == 0 else None
+    wpb = max(1, int(windows_per_batch))
+    for r0 in range(0, rounds, wpb):
+        rr = list(range(r0, min(rounds, r0 + wpb)))
+        ks = [r * world + rank for r in rr if r * world + rank < nwin]
+        d = None
+        if ks:
+            idx = [window_frame_indices(k, n) for k in ks]
+            uniq = sorted(set(i for row in idx for i in row))
+            pre = io.preprocess(frames[uniq].to(dev), size)
+            pos = {f: j for j, f in enumerate(uniq)}
+            x = torch.stack([pre[[pos[i] for i in row]] for row in idx], 0)
+            del pre
+            with torch.no_grad():
+                d = forward(x).float()  # [B, 32, H, W]
+            del x
+            d = io.resize_depth(d.flatten(0, 1), (h, w)).view(len(ks), INFER_LEN, h, w)
+        if world == 1:
+            for j, k in enumerate(ks):
+                sink.put(k, d[j])
+            continue
+        # every rank takes part in every round's gather (a rank without a window sends zeros)
+        buf = torch.zeros(len(rr), INFER_LEN, h, w, dtype=torch.float32, device=dev)
+        if d is not None:
+            buf[:len(ks)] = d
+        bufs = _gather_round(buf, rank, world, group)
+        if rank == 0:
+            for src in range(world):
+                for j, r in enumerate(rr):
+                    k = r * world + src
+                    if k < nwin:
+                        sink.put(k, bufs[src][j])
+    if rank != 0:
+        return None, target_fps
+    out = sink.result()
     depth_list = []
-    for k in range(len(starts)):
-        depth_list += [f.cpu().numpy() for f in out[k]]
+    for k in range(nwin):
+        depth_list += list(out[k])
     return stitch(depth_list, n), target_fps
