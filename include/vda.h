@@ -41,6 +41,7 @@ enum {
 
 /*
  * Fused epilogue of a GEMM / conv tile, applied to the fp32 accumulator `acc` of output (m, n):
+ *   acc = rstd[m] * (acc - mean[m] * ln_colsum[n])         (LayerNorm fold, when ln_stats is set)
  *   v = acc + bias[n] + rowbias[((m / rdiv) % rmod) * N + n]
  *   v = act(v)
  *   v = res[m*ldres + n] + res2[m*ldres2 + n] + gamma[n] * v      (each term optional)
@@ -59,6 +60,13 @@ typedef struct vda_epilogue {
   int32_t act;           /* VDA_ACT_*                                                  */
   int32_t store;         /* VDA_STORE_*                                                */
   int32_t ps_k, ps_cout, ps_hin, ps_win; /* pixel-shuffle geometry (store == 1)       */
+  /* LayerNorm folded into the GEMM (block.py:84,87 norm1 / norm2 feeding qkv / fc1): X is the raw
+   * row stream x, W holds gamma (.) W_ln, bias holds W_ln beta + b, ln_colsum[n] = sum_k W[n, k] (of the
+   * fp16 W actually used), and ln_stats[m] = (mean, rstd) of row m from vda_row_stats.  Then
+   * rstd (x W^T - mean colsum) + bias = LN(x) W_ln^T + b exactly in real arithmetic.  ln_stats holds
+   * an even number of rows (M rounded up to 2).  Row store only, no gamma, activation none/gelu/relu. */
+  const float* ln_stats;  /* [round_up(M, 2), 2] or NULL                              */
+  const float* ln_colsum; /* [N]                                                     */
 } vda_epilogue;
 
 /* Version / diagnostics. */
@@ -110,6 +118,14 @@ int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int3
  */
 int vda_layernorm(const void* x, int64_t ldx, void* y, const float* gamma, const float* beta,
                   int32_t rows, int32_t C, float eps, int32_t skip_period, void* stream);
+
+/*
+ * Per-row LayerNorm statistics for the LN-folded GEMM (vda_epilogue.ln_stats): stats[r] = (mean,
+ * 1/sqrt(var + eps)) of row r of X (rows of C halfs, row stride ldx), fp32, two-pass like
+ * vda_layernorm (same values).  Replaces the statistics half of block.py:84,87 (norm1 / norm2).
+ */
+int vda_row_stats(const void* x, int64_t ldx, float* stats, int32_t rows, int32_t C, float eps,
+                  void* stream);
 
 /*
  * GroupNorm over NHWC frames: X [F, S, C] half -> Y [F, S, C] half, `groups` groups of C/groups
@@ -241,6 +257,9 @@ int vda_debug_force_tile(int32_t cfg);
  * (100 MHz ticks) of the delayed half of the blocks (-1 = automatic).  Process-global; for tuning.
  */
 int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
+/* Tuning experiment: with groups > 1 every phased-GEMM block starts ((block / 8) % groups) / groups of
+ * the stagger ticks late (desynchronises the CUs' epilogue store bursts).  0 = off. */
+int vda_debug_gemm_desync(int32_t groups);
 
 /*
  * Tuning hook for the strip-tiled 3x3 conv: split every tile's input channels over nsplit work items

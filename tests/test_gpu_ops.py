@@ -496,3 +496,34 @@ def test_conv3x3_halo_fused_resize(BT, Cin, Hs, Ws, H, W, relu):
     if H * W >= 128 * 128:
         y_mat = ops.conv2d(ops.upsample_bilinear(xh, H, W), wh, **kw)
         assert torch.equal(y, y_mat)
+
+
+@pytest.mark.parametrize("M,N,K,act", [(4001, 3072, 1024, 0), (4001, 4096, 1024, ACT_GELU), (301, 384, 384, 0),
+                                       (300, 1536, 384, ACT_GELU), (43840, 1024, 1024, 0)])
+def test_gemm_layernorm_fold(M, N, K, act):
+    """norm1 / norm2 folded into qkv / fc1 (block.py:84,87): rstd (x W'^T - mean colsum) + b' with
+    W' = gamma (.) W, b' = W beta + b, stats from vda_row_stats, vs torch fp32 LayerNorm -> Linear."""
+    g = torch.Generator().manual_seed(M + N)
+    x = (torch.randn(M, K, generator=g) * 3 + torch.randn(M, 1, generator=g) * 2).half().float()  # row offsets
+    gam = 1 + 0.2 * torch.randn(K, generator=g)
+    bet = 0.1 * torch.randn(K, generator=g)
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    ref = F.linear(F.layer_norm(x, (K,), gam, bet, eps=1e-6), w, b)
+    if act == ACT_GELU:
+        ref = F.gelu(ref)
+    wg = (w * gam[None, :]).half()
+    c1 = wg.float().sum(1)
+    bb = w @ bet + b
+    st = ops.row_stats(h(x), 1e-6)
+    assert st.shape == ((M + 1) // 2 * 2, 2)
+    mean, var = x.mean(1), x.var(1, unbiased=False)
+    assert torch.allclose(st[:M, 0].cpu(), mean, atol=1e-4, rtol=1e-5)
+    assert torch.allclose(st[:M, 1].cpu(), (var + 1e-6).rsqrt(), rtol=1e-4)
+    y = ops.gemm(h(x), wg.to(DEV), bias=f32(bb), act=act, ln_stats=st, ln_colsum=f32(c1))
+    err = rel(y, ref)
+    # the unfused fp16 path for scale: LN output rounded to fp16, W rounded to fp16
+    y0 = ops.gemm(ops.layernorm(h(x), f32(gam), f32(bet), 1e-6), h(w), bias=f32(b), act=act)
+    err0 = rel(y0, ref)
+    print(f"LN-folded GEMM {M}x{N}x{K} act={act}: rel-L1 {err:.2e} (unfused fp16 path {err0:.2e})")
+    assert err < max(2 * err0, 2e-3)

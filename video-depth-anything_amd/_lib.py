@@ -17,12 +17,12 @@ TORCH_LIB_PATH = os.path.join(_HERE, "libvda_torch.so")  # TORCH_LIBRARY(vda) ov
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
     "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
-    "vda_groupnorm", "vda_groupnorm_workspace",
+    "vda_row_stats", "vda_groupnorm", "vda_groupnorm_workspace",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
-    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_strip_split",
+    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_strip_split",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -44,6 +44,7 @@ class Epilogue(ctypes.Structure):
         ("gamma", c_void_p), ("res", c_void_p), ("ldres", c_int64), ("res2", c_void_p),
         ("ldres2", c_int64), ("act", c_int32), ("store", c_int32), ("ps_k", c_int32),
         ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
+        ("ln_stats", c_void_p), ("ln_colsum", c_void_p),
     ]
 
 
@@ -61,6 +62,7 @@ def _declare(lib):
         "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P, L, P], I),
         "vda_conv2d_workspace": ([I, I, I, I, I, I, I, I], L),
         "vda_layernorm": ([P, L, P, P, P, I, I, F, I, P], I),
+        "vda_row_stats": ([P, L, P, I, I, F, P], I),
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
         "vda_groupnorm_workspace": ([I, I, I, I], L),
         "vda_spatial_attention": ([P, P, I, I, I, I, F, P], I),
@@ -82,6 +84,7 @@ def _declare(lib):
         "vda_depth_head_f32": ([P, P, P, P, P, P, P, P, I, I, I, I, I, I, P], I),
         "vda_debug_force_tile": ([I], I),
         "vda_debug_gemm_sched": ([I, I], I),
+        "vda_debug_gemm_desync": ([I], I),
         "vda_debug_strip_split": ([I], I),
     }
     for name, (args, res) in sig.items():

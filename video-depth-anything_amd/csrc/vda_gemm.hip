@@ -148,6 +148,12 @@ struct ConvLoader {
 template <int ACT>
 __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4 v) {
   const vda_epilogue& e = p.epi;
+  if (e.ln_stats) {  // LayerNorm folded into the GEMM: rstd * (acc - mean * colsum)
+    const float2 mr = *reinterpret_cast<const float2*>(e.ln_stats + 2L * m);
+    const f4 c1 = *reinterpret_cast<const f4*>(e.ln_colsum + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = mr.y * fmaf(-mr.x, c1[j], v[j]);
+  }
   if (e.bias) {
     f4 b = *reinterpret_cast<const f4*>(e.bias + n);
     v += b;
@@ -571,10 +577,15 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
 // their LDS-read segment and their MFMA segment.  Restaging a region is >= 2 phases after its
 // last read and the DMA wait is one phase before the first read of the new tile (the margins the
 // stagger needs).  Raw s_barrier + explicit waits only: nothing drains the DMA queue implicitly.
-template <int XR, int WR, bool CONV, int ACT, bool ROWB>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
+template <int XR, int WR, bool CONV, int ACT, bool ROWB, bool LNF>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
 __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem) {
   // ROWB: per-row bias support (a separate instantiation: its row-index division would otherwise
   // raise the register pressure of every phased GEMM past the spill point)
+  // LNF: LayerNorm folded into the GEMM (vda_epilogue.ln_stats / ln_colsum): X is the raw residual
+  // stream, W = gamma (.) W_ln, and the epilogue applies rstd * (acc - mean * colsum) + bias.  The
+  // tile's 256 (mean, rstd) pairs are staged into LDS by the prologue DMA (2 KiB after the operand
+  // buffers and the Phi table); colsum takes the prefetched gamma registers (gamma is not allowed).
+  static_assert(!(LNF && (ROWB || CONV)), "LNF: dense, no row bias");
   static_assert(XR * WR == 4 && (XR == 2 || XR == 4), "8 waves as XR (m) x 8/XR (n), wave tile 128 x 64");
   constexpr int BM = 128 * XR, BN = 128 * WR;
   constexpr int HALF = 128 * BK;            // halfs per 128-row region (16 KiB)
@@ -582,6 +593,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   // GELU / GEGLU epilogues read Phi from a 16-KiB LDS table (phi_table.h) staged in the prologue
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
   const float* phi_lds = reinterpret_cast<const float*>(smem + 2 * BUF);
+  h16* lnst_lds = smem + 2 * BUF + (TAB ? 8192 : 0);  // LNF: [256][2] fp32 (mean, rstd)
 
   // thread id laundered through a volatile move: every lane-derived address below is recomputed
   // per tile instead of being hoisted out of the persistent tile loop (and spilled across it)
@@ -742,6 +754,13 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     glds16(src, smem + 2 * BUF + wave * 512);
     glds16(src + 8192, smem + 2 * BUF + 4096 + wave * 512);
   }
+  if constexpr (LNF) {  // rows m0 .. m0+255 of [M, 2] fp32 (mean, rstd): 2 pieces of 128 rows, waves 0-1
+    if (wave < 2) {
+      const int r = m0 + wave * 128 + lane * 2;  // this lane's 16 B = rows r, r + 1 (M is even or row r+1 unused)
+      const void* src = r < p.M ? (const void*)(p.epi.ln_stats + (long)r * 2) : (const void*)g_zero_page;
+      glds16(src, lnst_lds + wave * 512);
+    }
+  }
   TS(1);
   stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
   if (nk > 1) {
@@ -766,7 +785,9 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       pbv[i] = f4{0.f, 0.f, 0.f, 0.f};
       pgv[i] = f4{1.f, 1.f, 1.f, 1.f};
       if (e.bias) pbv[i] = *reinterpret_cast<const f4*>(e.bias + (ACT == VDA_ACT_GEGLU ? (n0 + wn * 64 + (i & ~1) * 16 + nq0 < p.N ? n0 + wn * 64 + (i & ~1) * 16 + nq0 : 0) + (i & 1) * 16 : nc));
-      if (e.gamma) {
+      if constexpr (LNF) {
+        pgv[i] = *reinterpret_cast<const f4*>(e.ln_colsum + nc);  // sum_k W[n, k] (LN fold)
+      } else if (e.gamma) {
         if constexpr (ACT == VDA_ACT_GEGLU) {
           if (i % 2 == 0) pgv[i] = *reinterpret_cast<const f4*>(e.gamma + (n < p.N ? (n0 >> 1) + ((wn * 64 + i * 16) >> 1) + nq0 : 0));
         } else {
@@ -865,7 +886,19 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       nok[i] = n < p.N;
       ncl[i] = nok[i] ? n : 0;
     }
-    if (e.bias) {  // bias folded into the accumulators up front (GEGLU: h and g halves alike)
+    if constexpr (LNF) {  // y = rstd * (acc - mean * colsum) + bias (LayerNorm folded, before the activation)
+      const float* st = reinterpret_cast<const float*>(lnst_lds);
+      const f4* bv = pbv;  // zero when there is no bias
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float2 mr = *reinterpret_cast<const float2*>(st + 2 * (wm * 128 + j * 16 + mcol));
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            acc[i][j][r] = fmaf(mr.y, fmaf(-mr.x, pgv[i][r], acc[i][j][r]), bv[i][r]);
+      }
+    } else if (e.bias) {  // bias folded into the accumulators up front (GEGLU: h and g halves alike)
       f4 bv[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -992,7 +1025,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     // here, before phase 1, so its 16 loads per thread overlap the activation / LDS staging instead
     // of stalling phase 2 four times per tile (in situ, proj ran 45 % over its residual-free time).
     // The residual may alias the output: this tile is written only by this block, in phase 2.
-    constexpr bool RPF = XR == 2 && ACT == VDA_ACT_NONE && !CONV && !ROWB;  // NIT = 16 chunks = 64 VGPRs; the
+    constexpr bool RPF = XR == 2 && ACT == VDA_ACT_NONE && !CONV && !ROWB && !LNF;  // NIT = 16 chunks = 64 VGPRs; the
     // other instantiations have no register room for it (GELU / GEGLU / conv / row bias: spills)
     h8 rpre[RPF ? NIT : 1];
     if constexpr (RPF) {
@@ -1004,7 +1037,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           rpre[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, vr + it * sr, 0, 0));
       }
     }
-    if (e.gamma) phase1(std::true_type{});
+    if (!LNF && e.gamma) phase1(std::true_type{});
     else phase1(std::false_type{});
     __syncthreads();
     TS(4);
@@ -1099,25 +1132,30 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
 // the blocks that own one tile fewer start half a tile late (stagger_ticks of the 100 MHz
 // s_memrealtime clock): the bursts of the two halves then overlap the other half's main loop, and
 // the delayed blocks still finish no later than the blocks with the extra tile.
-template <int XR, int WR, bool CONV, int ACT, bool ROWB>
-__global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n, int stagger_ticks) {
+template <int XR, int WR, bool CONV, int ACT, bool ROWB, bool LNF = false>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m, int tiles_n, int stagger_ticks,
+                                                      int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0)];
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0) + (LNF ? 1024 : 0)];
   const int ntiles = tiles_m * tiles_n;
-  if (stagger_ticks > 0 && (int)blockIdx.x >= ntiles % (int)gridDim.x && ((blockIdx.x >> 3) & 1)) {
+  if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
+    const uint64_t d = (uint64_t)(((blockIdx.x >> 3) % desync) * stagger_ticks / desync);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < d) __builtin_amdgcn_s_sleep(16);
+  } else if (stagger_ticks > 0 && (int)blockIdx.x >= ntiles % (int)gridDim.x && ((blockIdx.x >> 3) & 1)) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)stagger_ticks) __builtin_amdgcn_s_sleep(16);
   }
   if constexpr (CONV) {  // convs launch one block per tile (phased_sched): no loop-carried state
     const int vb = blockIdx.x;
     TS(0);
-    gemm256_tile<XR, WR, CONV, ACT, ROWB>(p, vb, tiles_m, tiles_n, smem);
+    gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF>(p, vb, tiles_m, tiles_n, smem);
     TS(7);
   } else {
     for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
       TS(0);
-      gemm256_tile<XR, WR, CONV, ACT, ROWB>(p, vb, tiles_m, tiles_n, smem);
+      gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF>(p, vb, tiles_m, tiles_n, smem);
       __syncthreads();
       TS(7);
     }
@@ -1126,6 +1164,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
 
 int g_force_tile = -1;  // debug / tuning override (vda_debug_force_tile)
 int g_persist = -1, g_stagger = -1;  // debug overrides (vda_debug_gemm_sched); -1 = automatic
+int g_desync = 0;                     // tuning experiment (vda_debug_gemm_desync)
 
 int cu_count() {
   static int cached[64] = {0};
@@ -1170,11 +1209,20 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
   phased_sched(tiles_m * tiles_n, (p.K + 63) / 64, CONV, grid, ticks);
   if constexpr (!CONV && ACT == VDA_ACT_NONE) {
     if (p.epi.rowbias) {
-      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks);
+      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks,
+                         g_desync);
       return;
     }
   }
-  hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks);
+  if constexpr (!CONV && XR == 2 && (ACT == VDA_ACT_NONE || ACT == VDA_ACT_GELU)) {
+    if (p.epi.ln_stats) {
+      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n,
+                         ticks, g_desync);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks,
+                     g_desync);
 }
 
 template <bool CONV, int ACT>
@@ -1195,7 +1243,7 @@ void launch_act(const GemmParams& p, hipStream_t st) {
                           (!e.rowbias || (!CONV && ACT == VDA_ACT_NONE));
     if (p.N <= 64 || (p.K <= 256 && p.N < 256)) cfg = 2;
     else if (p.N >= 256 && p.M >= 4096 && dense_ok && (e.store != VDA_STORE_ROWS || a16)) cfg = 4;
-    else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS) cfg = 5;
+    else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS && !e.ln_stats) cfg = 5;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
     else cfg = 0;
@@ -1256,6 +1304,9 @@ int check_epi(const vda_epilogue& e, int N) {
                 (e.store == VDA_STORE_PIXEL_SHUFFLE && e.ps_k > 0 && e.ps_cout > 0 && e.ps_cout % 4 == 0 &&
                  e.ps_hin > 0 && e.ps_win > 0 && N == e.ps_k * e.ps_k * e.ps_cout && !e.res && !e.res2),
                 "bad pixel-shuffle store geometry");
+  VDA_CHECK_ARG(!e.ln_stats || (e.ln_colsum && e.store == VDA_STORE_ROWS && !e.gamma &&
+                                 (e.act == VDA_ACT_NONE || e.act == VDA_ACT_GELU || e.act == VDA_ACT_RELU)),
+                "ln_stats needs ln_colsum, a row store, no gamma, activation none / gelu / relu");
   VDA_CHECK_ARG(!e.res || e.ldres % 4 == 0, "ldres % 4");
   VDA_CHECK_ARG(!e.res2 || e.ldres2 % 4 == 0, "ldres2 % 4");
   return 0;
@@ -1416,6 +1467,11 @@ extern "C" int64_t vda_depth_head_workspace(int32_t BT, int32_t Hin, int32_t Win
 
 extern "C" int vda_debug_force_tile(int32_t cfg) {
   g_force_tile = cfg;
+  return 0;
+}
+
+extern "C" int vda_debug_gemm_desync(int32_t groups) {
+  g_desync = groups;
   return 0;
 }
 

@@ -59,6 +59,43 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const h16* __restrict__ 
   }
 }
 
+// Row statistics only (the LN-folded GEMM, vda_epilogue.ln_stats): the same two-pass mean / rstd as
+// layernorm_kernel, one wave per row, written as float2.  Reads the row once, writes 8 bytes.
+__global__ __launch_bounds__(256) void row_stats_kernel(const h16* __restrict__ x, long ldx, float2* __restrict__ st,
+                                                        int rows, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const h16* xr = x + (long)row * ldx;
+  const int nch = C >> 3;
+  float v[4][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+      h8 t = __builtin_bit_cast(h8, ldg16(xr + c * 8));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { v[i][j] = (float)t[j]; s += v[i][j]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[i][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { float d = v[i][j] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)C + eps);
+  if (lane == 0) st[row] = make_float2(mean, rstd);
+}
+
 // Narrow rows (C <= 512, the motion modules' C = 256 / 128): one wave would leave lanes idle and
 // wait on one 512-B row, so LPR = C / 8 lanes own a row (one 16-B chunk each) and a wave normalises
 // 64 / LPR rows; the same two-pass statistics, reduced over the row's LPR lanes only.
@@ -270,6 +307,17 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x
 }
 
 }  // namespace
+
+extern "C" int vda_row_stats(const void* x, int64_t ldx, float* stats, int32_t rows, int32_t C, float eps,
+                             void* stream) {
+  VDA_CHECK_ARG(x && stats, "null pointer");
+  VDA_CHECK_ARG(rows > 0 && C > 0 && C % 8 == 0 && C <= 2048, "C must be a multiple of 8, <= 2048");
+  VDA_CHECK_ARG(ldx % 8 == 0 && ldx >= C, "ldx must be a multiple of 8 and >= C");
+  hipLaunchKernelGGL(row_stats_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const h16*)x, (long)ldx,
+                     (float2*)stats, rows, C, eps);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int vda_layernorm(const void* x, int64_t ldx, void* y, const float* gamma, const float* beta,
                              int32_t rows, int32_t C, float eps, int32_t skip_period, void* stream) {

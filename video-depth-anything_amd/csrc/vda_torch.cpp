@@ -59,7 +59,8 @@ const void* ptr(OptT t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
 // vda_epilogue from the optional per-channel / per-row / residual operands (include/vda.h).
 vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma, OptT res,
-                      OptT res2, int64_t act, at::ScalarType dt) {
+                      OptT res2, int64_t act, at::ScalarType dt, OptT ln_stats = c10::nullopt,
+                      OptT ln_colsum = c10::nullopt) {
   vda_epilogue e;
   std::memset(&e, 0, sizeof(e));
   if (bias) need_contig(*bias, at::kFloat, "bias", x);
@@ -84,12 +85,21 @@ vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, in
   }
   e.act = (int32_t)act;
   e.store = VDA_STORE_ROWS;
+  if (ln_stats) {
+    TORCH_CHECK(ln_colsum.has_value(), "vda gemm: ln_stats needs ln_colsum");
+    need_contig(*ln_stats, at::kFloat, "ln_stats", x);
+    need_contig(*ln_colsum, at::kFloat, "ln_colsum", x);
+    TORCH_CHECK(ln_stats->dim() == 2 && ln_stats->size(1) == 2 && ln_stats->size(0) >= (x.size(0) + 1) / 2 * 2,
+                "vda gemm: ln_stats must be [round_up(M, 2), 2] (from vda.row_stats)");
+    e.ln_stats = (const float*)ln_stats->data_ptr();
+    e.ln_colsum = (const float*)ln_colsum->data_ptr();
+  }
   return e;
 }
 
 // ---- linear / 1x1 conv / ConvTranspose(k=s) ------------------------------------------------------
 Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-                 OptT res, OptT res2, int64_t act, Tensor out) {
+                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, Tensor out) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "vda gemm: x must be a 2-D row-major (possibly row-strided) matrix");
   need_contig(w, dt, "w", x);
@@ -101,7 +111,7 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
               "vda gemm: out must be [", M, ", ", nout, "] ", dt, " with unit column stride");
   if (x.is_meta()) return out;
   const at::OptionalDeviceGuard g(x.device());
-  vda_epilogue e = make_epi(x, bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt);
+  vda_epilogue e = make_epi(x, bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt, ln_stats, ln_colsum);
   const int rc = dt == at::kHalf
                      ? vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), (int32_t)M,
                                 (int32_t)N, (int32_t)K, &e, stream_of(x))
@@ -113,17 +123,17 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
 }
 
 Tensor gemm(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-            OptT res, OptT res2, int64_t act) {
+            OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "vda gemm: x and w must be 2-D");
   const int64_t nout = act == VDA_ACT_GEGLU ? w.size(0) / 2 : w.size(0);
   Tensor out = at::empty({x.size(0), nout}, x.options().dtype(dt));
-  return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, out);
+  return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, out);
 }
 
 Tensor& gemm_out(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-                 OptT res, OptT res2, int64_t act, Tensor& out) {
-  gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, out);
+                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, Tensor& out) {
+  gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, out);
   return out;
 }
 
@@ -216,6 +226,20 @@ Tensor layernorm(const Tensor& x, const Tensor& gamma, const Tensor& beta, doubl
                                          (const float*)gamma.data_ptr(), (const float*)beta.data_ptr(), (int32_t)nr,
                                          (int32_t)C, (float)eps, (int32_t)skip_period, stream_of(x));
   check_rc(rc, "vda_layernorm");
+  return out;
+}
+
+// [round_up(R, 2), 2] fp32 (mean, rstd) per row: the statistics half of a LayerNorm, for the LN-folded GEMM
+Tensor row_stats(const Tensor& x, double eps) {
+  TORCH_CHECK(x.scalar_type() == at::kHalf && x.dim() == 2 && x.stride(1) == 1,
+              "vda row_stats: x must be a 2-D row-major fp16 matrix");
+  const int64_t R = x.size(0), C = x.size(1);
+  Tensor out = at::empty({(R + 1) / 2 * 2, 2}, x.options().dtype(at::kFloat));
+  if (x.is_meta()) return out;
+  const at::OptionalDeviceGuard g(x.device());
+  check_rc(vda_row_stats(x.data_ptr(), x.stride(0), (float*)out.data_ptr(), (int32_t)R, (int32_t)C, (float)eps,
+                         stream_of(x)),
+           "vda_row_stats");
   return out;
 }
 
@@ -380,9 +404,12 @@ Tensor depth_resize(const Tensor& depth, int64_t ho, int64_t wo) {
 
 TORCH_LIBRARY(vda, m) {
   m.def("gemm(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
-        "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0) -> Tensor");
+        "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
+        "Tensor? ln_colsum=None) -> Tensor");
   m.def("gemm.out(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
-        "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, *, Tensor(a!) out) -> Tensor(a!)");
+        "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
+        "Tensor? ln_colsum=None, *, Tensor(a!) out) -> Tensor(a!)");
+  m.def("row_stats(Tensor x, float eps) -> Tensor");
   m.def("conv_transpose_ks(Tensor x, Tensor w, Tensor bias, int BT, int h, int w_, int k) -> Tensor");
   m.def("conv2d(Tensor x, Tensor w, int ks=3, int stride=1, int pad=1, Tensor? bias=None, bool pre_relu=False, "
         "int act=0, Tensor? res=None, Tensor? res2=None, int[]? up=None) -> Tensor");
@@ -404,6 +431,7 @@ TORCH_LIBRARY(vda, m) {
     m.impl("conv_transpose_ks", &conv_transpose_ks);          \
     m.impl("conv2d", &conv2d);                                \
     m.impl("layernorm", &layernorm);                          \
+    m.impl("row_stats", &row_stats);                          \
     m.impl("groupnorm", &groupnorm);                          \
     m.impl("spatial_attention", &spatial_attention);          \
     m.impl("temporal_attention", &temporal_attention);        \

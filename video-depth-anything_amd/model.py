@@ -16,6 +16,7 @@ accumulation, statistics and depth tail (dpt_temporal.py:95-97 keeps output_conv
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -289,17 +290,36 @@ class VideoDepthAnything(nn.Module):
         P.cls = _f(enc.cls_token.reshape(C)).to(dev)
         P.pos = _f(enc.pos_embed).to(dev)
         P.blocks = []
+        # fp16 mode folds norm1 / norm2 into the qkv / fc1 GEMMs (block.py:84,87): W' = gamma (.) W,
+        # b' = W beta + b, colsum = sum_k W' (of the fp16 W' the kernel multiplies); the GEMM epilogue
+        # applies rstd * (x W'^T - mean colsum) + b' from per-row statistics (vda_row_stats), so the
+        # normalised copy of the token tensor is never written or re-read.
+        P.lnfold = not fp32 and os.environ.get("VDA_NO_LNFOLD", "0") != "1"
+
+        def _ln_fold(lin, ln):
+            w = lin.weight.detach().float()
+            wg = (w * ln.weight.detach().float()[None, :]).to(wd).contiguous()
+            c1 = wg.float().sum(1).contiguous()
+            bb = (w @ ln.bias.detach().float() + lin.bias.detach().float()).contiguous()
+            return wg.to(dev), c1.to(dev), bb.to(dev)
+
         for b in enc.blocks:
             q = _Packed()
             q.n1w, q.n1b = _f(b.norm1.weight).to(dev), _f(b.norm1.bias).to(dev)
-            q.qkv_w, q.qkv_b = _h(b.attn.qkv.weight).to(dev), _f(b.attn.qkv.bias).to(dev)
+            if P.lnfold:
+                q.qkv_w, q.qkv_c1, q.qkv_b = _ln_fold(b.attn.qkv, b.norm1)
+            else:
+                q.qkv_w, q.qkv_b = _h(b.attn.qkv.weight).to(dev), _f(b.attn.qkv.bias).to(dev)
             # LayerScale folded into the projections (gamma * (W h + b) = (gamma W) h + gamma b): the
             # GEMM epilogue then carries no per-channel multiply (block.py ls1 / ls2)
             g1 = b.ls1.gamma.detach().float()
             q.proj_w = _h(b.attn.proj.weight.detach().float() * g1[:, None]).to(dev)
             q.proj_b = _f(b.attn.proj.bias.detach().float() * g1).to(dev)
             q.n2w, q.n2b = _f(b.norm2.weight).to(dev), _f(b.norm2.bias).to(dev)
-            q.fc1_w, q.fc1_b = _h(b.mlp.fc1.weight).to(dev), _f(b.mlp.fc1.bias).to(dev)
+            if P.lnfold:
+                q.fc1_w, q.fc1_c1, q.fc1_b = _ln_fold(b.mlp.fc1, b.norm2)
+            else:
+                q.fc1_w, q.fc1_b = _h(b.mlp.fc1.weight).to(dev), _f(b.mlp.fc1.bias).to(dev)
             g2 = b.ls2.gamma.detach().float()
             q.fc2_w = _h(b.mlp.fc2.weight.detach().float() * g2[:, None]).to(dev)
             q.fc2_b = _f(b.mlp.fc2.bias.detach().float() * g2).to(dev)
@@ -473,13 +493,19 @@ class VideoDepthAnything(nn.Module):
         feats: List[torch.Tensor] = []
         cls: Optional[List[torch.Tensor]] = [] if self.use_clstoken else None
         for i, q in enumerate(P.blocks):
-            hN = ops.layernorm(tok, q.n1w, q.n1b, 1e-6)
-            qkv = ops.gemm(hN, q.qkv_w, bias=q.qkv_b)
+            if P.lnfold:  # norm1 folded into the qkv GEMM (statistics only: 8 bytes per token)
+                qkv = ops.gemm(tok, q.qkv_w, bias=q.qkv_b, ln_stats=ops.row_stats(tok, 1e-6), ln_colsum=q.qkv_c1)
+            else:
+                qkv = ops.gemm(ops.layernorm(tok, q.n1w, q.n1b, 1e-6), q.qkv_w, bias=q.qkv_b)
             at = ops.spatial_attention(qkv, BT, ntok, P.heads, 64)
             del qkv
             ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok)
-            hN = ops.layernorm(tok, q.n2w, q.n2b, 1e-6)
-            f = ops.gemm(hN, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, tag="enc_fc1")
+            if P.lnfold:  # norm2 folded into the fc1 GEMM
+                f = ops.gemm(tok, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, ln_stats=ops.row_stats(tok, 1e-6),
+                             ln_colsum=q.fc1_c1, tag="enc_fc1")
+            else:
+                f = ops.gemm(ops.layernorm(tok, q.n2w, q.n2b, 1e-6), q.fc1_w, bias=q.fc1_b, act=ACT_GELU,
+                             tag="enc_fc1")
             ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok)
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)

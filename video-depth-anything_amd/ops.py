@@ -55,9 +55,11 @@ def _need(t: Tensor, dtype, name: str):
 
 
 def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
-         res2=None, act=ACT_NONE, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
+         res2=None, act=ACT_NONE, ln_stats=None, ln_colsum=None, out: Optional[Tensor] = None,
+         tag: Optional[str] = None) -> Tensor:
     """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view.
-    fp16 x/w -> vda_gemm; fp32 x/w -> vda_gemm_f32 (fp32 mode).  torch.ops.vda.gemm[.out]."""
+    fp16 x/w -> vda_gemm; fp32 x/w -> vda_gemm_f32 (fp32 mode).  torch.ops.vda.gemm[.out].
+    ``ln_stats`` (from ``row_stats``) + ``ln_colsum`` fold a LayerNorm of x into the GEMM (vda.h)."""
     _need(x, x.dtype, "x")
     probe = _PROBE is not None and tag in _PROBE
     if probe:
@@ -65,9 +67,10 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
         ev0.record()
     v = _vda()
     if out is None:
-        out = v.gemm(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act))
+        out = v.gemm(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum)
     else:
-        v.gemm.out(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), out=out)
+        v.gemm.out(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum,
+                   out=out)
     if probe:
         ev1.record()
         _PROBE[tag].append((ev0, ev1, 2.0 * x.shape[0] * w.shape[0] * x.shape[1]))
@@ -96,6 +99,12 @@ def layernorm(x: Tensor, gamma: Tensor, beta: Tensor, eps: float, *, skip_period
     """Row LayerNorm of x [R, C] (row-strided ok).  skip_period=np drops each frame's cls row."""
     _need(x, x.dtype, "x")
     return _vda().layernorm(x, gamma, beta, float(eps), int(skip_period), rows)
+
+
+def row_stats(x: Tensor, eps: float) -> Tensor:
+    """Per-row LayerNorm statistics of x [R, C] fp16: [round_up(R, 2), 2] fp32 (mean, rstd)."""
+    _need(x, torch.float16, "x")
+    return _vda().row_stats(x, float(eps))
 
 
 def groupnorm(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, eps: float) -> Tensor:
