@@ -268,6 +268,13 @@ int vda_debug_gemm_desync(int32_t groups);
  */
 int vda_debug_strip_split(int32_t nsplit);
 
+/*
+ * Tuning hook for the halo-tiled phased 3x3 conv (Cout = 256, csrc/vda_hconv.hip): -1 = automatic
+ * (maps of >= 128^2 pixels), 0 = never (implicit GEMM / strip conv), 1 = every shape it serves.
+ * Process-global; for tests and A/B runs.
+ */
+int vda_debug_hconv(int32_t mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -527,3 +527,46 @@ def test_gemm_layernorm_fold(M, N, K, act):
     err0 = rel(y0, ref)
     print(f"LN-folded GEMM {M}x{N}x{K} act={act}: rel-L1 {err:.2e} (unfused fp16 path {err0:.2e})")
     assert err < max(2 * err0, 2e-3)
+
+
+@pytest.mark.parametrize("Cin,H,W,BT,mode", [(256, 148, 148, 2, "rcu2"), (256, 148, 148, 2, "rcu1"), (256, 74, 74, 3, "plain"),
+                                             (64, 9, 33, 2, "rcu2"), (128, 17, 40, 1, "rcu1"), (512, 8, 32, 2, "plain"),
+                                             (64, 1, 1, 3, "rcu2"), (256, 37, 150, 1, "rcu2")])
+def test_conv3x3_hconv_cout256(Cin, H, W, BT, mode):
+    """3x3 / 256-output convs on the halo-tiled phased kernel (csrc/vda_hconv.hip; the refinenet RCU
+    convs and layer1_rn, blocks.py:68-91, dpt.py:100-104): 8 x 32 tiles with partial edge tiles,
+    patches clipped at every border, 1 .. 8 channel slabs, pre-ReLU + ReLU (RCU conv1), bias + skip
+    + fusion adds (RCU conv2).  vs torch fp32, and vs the implicit-GEMM conv (fp32 accumulation in
+    another K order: not bit-identical)."""
+    x = rnd(BT, Cin, H, W, seed=290)
+    w, b = rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=291), rnd(256, scale=0.1, seed=292)
+    r1, r2 = rnd(BT, 256, H, W, seed=293), rnd(BT, 256, H, W, seed=294)
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    kw = {}
+    if mode == "plain":
+        ref = F.conv2d(x, w, padding=1)
+    elif mode == "rcu1":
+        ref = F.relu(F.conv2d(F.relu(x), w, b, padding=1))
+        kw = dict(bias=f32(b), pre_relu=True, act=ACT_RELU)
+    else:
+        ref = F.conv2d(x, w, b, padding=1) + r1 + r2
+        kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
+    ref = ref.permute(0, 2, 3, 1)
+    xh, wh = nh(x), nh(w)
+    lib = vda_amd._libvda()
+    lib.vda_debug_hconv(1)
+    try:
+        y = ops.conv2d(xh, wh, **kw)
+        y_again = ops.conv2d(xh, wh, **kw)
+    finally:
+        lib.vda_debug_hconv(-1)
+    assert rel(y, ref) < 2e-3
+    assert torch.equal(y, y_again)
+    lib.vda_debug_hconv(0)
+    lib.vda_debug_force_tile(-2)
+    try:
+        y2 = ops.conv2d(xh, wh, **kw)
+    finally:
+        lib.vda_debug_force_tile(-1)
+        lib.vda_debug_hconv(-1)
+    assert rel(y, y2) < 1e-3

@@ -51,6 +51,10 @@ int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const f
                          float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st);
 int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int Hs, int Ws,
                         int H, int W, int Cin, int Cout, hipStream_t st);
+// halo-tiled phased 3x3 conv, Cout = 256 (vda_hconv.hip)
+bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout);
+int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st);
 
 namespace {
 
@@ -1345,6 +1349,7 @@ static bool conv_takes_strip(int BT, int H, int W, int Cin, int Cout, int ks, in
 extern "C" int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
                                         int32_t stride, int32_t pad) {
   if (BT <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  if (ks == 3 && stride == 1 && pad == 1 && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout)) return 0;
   if (!conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0)) return 0;
   return vda_conv_strip_ws_bytes(BT, H, W, Cin, Cout);
 }
@@ -1384,6 +1389,14 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
       if (rc != 1) return rc;
     }
     return launch_reg_conv(p, (hipStream_t)stream);
+  }
+  // large maps with 256 output channels (the refinenet RCU convs and layer1_rn at 148^2): the
+  // halo-tiled phased conv stages each input patch once per 64-channel slab instead of 9 times
+  if (ks == 3 && stride == 1 && pad == 1 && !p.epi.gamma && !p.epi.rowbias && (!p.epi.res || p.epi.ldres == Cout) &&
+      (!p.epi.res2 || p.epi.ldres2 == Cout) && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout)) {
+    rc = vda_conv_hconv(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, BT, H, W,
+                        Cin, Cout, (hipStream_t)stream);
+    if (rc != 1) return rc;
   }
   if (conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0) && !p.epi.gamma && !p.epi.rowbias &&
       (!p.epi.res || p.epi.ldres == Cout) && (!p.epi.res2 || p.epi.ldres2 == Cout)) {

@@ -1,0 +1,365 @@
+// Halo-tiled 3x3 conv with 256 output channels on the phased 256x256 MFMA main loop (gfx950).
+//
+// Serves the FeatureFusionBlock RCU convs and layerN_rn convs at the large decoder maps
+// (util/blocks.py:68-91 ResidualConvUnit, dpt.py:100-104 scratch.layerN_rn; 148^2 and 74^2 for a
+// 518^2 input): y = act(conv3x3(pre_relu ? relu(x) : x) + bias) + res + res2, NHWC fp16.
+//
+// The implicit-GEMM conv (vda_gemm.hip) re-gathers every input pixel once per tap: its 256-pixel
+// X tile is refetched 9 times per 64-channel slab, and with Cout = 256 there is a single N tile, so
+// nothing else amortises those bytes (~5x the map in fabric reads, K steps at ~2x the dense GEMM's).
+// Here a block owns an 8 x 32 output tile (256 pixels) and stages its 10 x 34 input patch ONCE per
+// 64-channel slab by LDS-DMA (43 KiB, spread over the first 6 K steps of the previous slab); all 9
+// taps read their X fragments out of the patch at a tap offset.  Per K step (one tap of one slab)
+// only the 32-KiB W tile is streamed, exactly as in the dense phased GEMM:
+//
+//   8 waves = 2 (m) x 4 (n), wave tile 128 pixels x 64 channels, v_mfma_f32_16x16x32_f16 with W as
+//   the A operand; two W buffers of four quarters, each refilled in its own phase by
+//   buffer_load ... lds (P2: Wq0(t+1) -> other buffer, P4: Wq1(t+2) -> this buffer), waves 4-7 one
+//   barrier behind, one counted vmcnt per K step, raw s_barrier only.  Patch pieces of slab s+1 are
+//   issued in P1 of steps 0..5 of slab s and retired by the same step's P4 wait; the slot they fill
+//   was last read in P3 of the previous slab's last step (2 phases earlier, the stagger margin).
+//
+// LDS: 2 x 32 KiB W + 2 x 43 KiB patch = 150 KiB; the fp16 output tile (128 KiB) is staged over it
+// in the epilogue and written as whole 512-B pixel rows.  Patch slot layout: pixel p's 16-B chunk c
+// at p * 128 B + ((c ^ (p & 7)) * 16): for the ds_read_b128 lane groups (16 consecutive pixels of
+// one tile row, chunks c / c + 1) the 16 accesses of a group hit 16 distinct (p & 1, chunk ^ (p & 7))
+// bank quads at any tap offset, i.e. conflict-free.
+#include "vda_common.h"
+#include "../../include/vda.h"
+
+namespace {
+
+constexpr int HC_TR = 8, HC_TC = 32;                 // output tile rows x columns
+constexpr int HC_PC = HC_TC + 2;                     // patch width (34)
+constexpr int HC_NPIX = (HC_TR + 2) * HC_PC;         // 340 patch pixels
+constexpr int HC_PP = (HC_NPIX * 8 + 63) / 64;       // 43 one-KiB DMA pieces per 64-channel slab
+constexpr int HC_PSLOT = HC_PP * 512;                // halfs per patch slot
+constexpr int HC_PPW = (HC_PP + 7) / 8;              // patch pieces per wave (6; waves 3-7 own 5)
+constexpr int HC_BK = 64;
+constexpr int HC_HALF = 128 * HC_BK;                 // halfs per 128-row W region
+constexpr int HC_WBUF = 2 * HC_HALF;                 // one K step of W (256 rows)
+static_assert(HC_PPW <= 9, "patch pieces are issued in the first steps of a slab");
+
+__device__ __attribute__((aligned(64))) uint4 g_hc_zero[4];
+
+__device__ __forceinline__ int hc_swz(int row, int chunk) { return row * HC_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
+
+template <int N>
+__device__ __forceinline__ void hc_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+struct HconvArgs {
+  const h16* x;     // [BT, H, W, Cin]
+  const h16* w;     // [256, 3, 3, Cin]
+  h16* y;           // [BT, H, W, 256]
+  const float* bias;
+  const h16* res;   // [BT, H, W, 256] or null
+  const h16* res2;
+  int H, W, Cin, relu_out;
+  int tiles_x, tiles_y, ntiles;
+};
+
+template <bool PRE>
+__global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * HC_WBUF + 2 * HC_PSLOT];
+  h16* const wsm = smem;
+  h16* const psm = smem + 2 * HC_WBUF;
+
+  int tid;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+
+  // XCD-aware tile order: the blocks of one XCD take a contiguous run of tiles (neighbours share
+  // patch rows and the whole W in that XCD's L2)
+  int bt, y0, x0;
+  {
+    const int bid = blockIdx.x, nwg = a.ntiles;
+    const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+    const int t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+    const int tx = t % a.tiles_x;
+    const int rr = t / a.tiles_x;
+    y0 = (rr % a.tiles_y) * HC_TR;
+    x0 = tx * HC_TC;
+    bt = rr / a.tiles_y;
+  }
+  const int H = a.H, W = a.W, Cin = a.Cin;
+  const int K = 9 * Cin;
+  const int nslab = Cin / 64;
+  const int NK = 9 * nslab;
+  const h16* xf0 = a.x + (long)bt * H * W * Cin;
+
+  // this lane's patch pieces: element offset (slab 0) within the frame, -1 = zero (padding / unused)
+  int poff[HC_PPW];
+#pragma unroll
+  for (int j = 0; j < HC_PPW; ++j) {
+    const int q = wave + 8 * j;
+    const int p = q * 8 + (lane >> 3);
+    const int cd = (lane & 7) ^ (p & 7);
+    const int pr = p / HC_PC, pc = p - pr * HC_PC;
+    const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
+    poff[j] = (q < HC_PP && p < HC_NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+                  ? (iy * W + ix) * Cin + cd * 8
+                  : -1;
+  }
+  auto patch_piece = [&](int slab, int j) {
+    const int q = wave + 8 * j;
+    if (q < HC_PP) {
+      const void* src = poff[j] >= 0 ? (const void*)(xf0 + poff[j] + slab * 64) : (const void*)g_hc_zero;
+      __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)(psm + (slab & 1) * HC_PSLOT + q * 512), 16, 0, 0);
+    }
+  };
+
+  // W quarters (as the phased GEMM): quarter i = rows {32i..32i+31, 64+32i..64+32i+31} of each
+  // 128-row region; wave w moves one 8-row piece per region, per-lane constant byte offset, the
+  // K-step offset (tap * Cin + slab * 64 halfs) in soffset
+  auto wr_of = [&](int i) { return (wave >> 2) * 64 + i * 32 + (wave & 3) * 8 + (lane >> 3); };
+  const int kch0 = ((lane & 7) ^ ((((wave & 1) << 3 | (lane >> 3)) >> 1) & 7)) * 8;
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, (int)(256L * K * 2), 0x00020000);
+  unsigned wvo[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) wvo[hh][i] = (unsigned)(((hh * 128 + wr_of(i)) * K + kch0) * 2);
+  auto koff = [&](int kt) {
+    const int slab = kt / 9, tap = kt - slab * 9;
+    return (tap * Cin + slab * 64) * 2;
+  };
+  auto stage_w = [&](int kt, int buf, int i) {
+    const int so = koff(kt);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          wrs, (VDA_LDS void*)(wsm + buf * HC_WBUF + hh * HC_HALF + (wr_of(i) - (lane >> 3)) * HC_BK), 16,
+          (int)wvo[hh][i], so, 0, 0);
+  };
+
+  f4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: slab 0's patch, all of W(0), W(1) quarter 1 (the loop expects it from "step -1")
+#pragma unroll
+  for (int j = 0; j < HC_PPW; ++j) patch_piece(0, j);
+  stage_w(0, 0, 0);
+  stage_w(0, 0, 1);
+  if (NK > 1) {
+    stage_w(1, 1, 1);
+    hc_wait<2>();
+  } else {
+    hc_wait<0>();
+  }
+  __builtin_amdgcn_s_barrier();
+  // PRE (the RCU's relu(x) input): the patch is rectified once in LDS after it lands (2 passes per
+  // slab in P2 of the slab's steps 7 and 8, 3 16-B slots per thread each), not per fragment read
+  // (each patch value feeds 9 taps x 4 n-waves)
+  auto relu_pass = [&](int slot, int part) {
+    h16* ps = psm + slot * HC_PSLOT;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int sl = tid + 512 * (3 * part + k);
+      if (sl < HC_PP * 64) {
+        h8* pp = reinterpret_cast<h8*>(ps + sl * 8);
+        *pp = relu8(*pp);
+      }
+    }
+  };
+  if (PRE) {
+    relu_pass(0, 0);
+    relu_pass(0, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  const bool lagging = wave >= 4;
+  if (lagging) __builtin_amdgcn_s_barrier();
+
+  const int frow = lane & 15, fchunk = lane >> 4;
+  const int woff = (wn >> 1) * HC_HALF;  // wave's 128-row W region
+  const int wrow0 = (wn & 1) * 64;
+  h8 xf[4][2], wf[2][2];
+  // X fragments of quadrant qm (m-blocks wm*8 + qm*4 + j = tile row wm*4 + qm*2 + (j >> 1), columns
+  // (j & 1) * 16 + frow) at tap offset toff = dy * 34 + dx, from patch slot ps
+  auto load_x = [&](const h16* ps, int toff, int qm) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = (wm * 4 + qm * 2 + (j >> 1)) * HC_PC + (j & 1) * 16 + frow + toff;
+      const int c0 = fchunk ^ (p & 7);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        xf[j][ks] = *reinterpret_cast<const h8*>(&ps[p * 64 + ((c0 ^ (4 * ks)) << 3)]);
+      }
+    }
+  };
+  auto load_w = [&](const h16* base, int qn) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        wf[i][ks] = *reinterpret_cast<const h8*>(&base[woff + hc_swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
+  };
+  auto mma = [&](int qm, int qn) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[qn * 2 + i][qm * 4 + j] = mfma16(wf[i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  for (int kt = 0; kt < NK; ++kt) {
+    const int cb = kt & 1, nb = cb ^ 1;
+    const int slab = kt / 9, tap = kt - slab * 9;
+    const int toff = (tap / 3) * HC_PC + (tap % 3);
+    const h16* ps = psm + (slab & 1) * HC_PSLOT;
+    const h16* base = wsm + cb * HC_WBUF;
+    const bool more1 = kt + 1 < NK, more2 = kt + 2 < NK;
+    // P1 (+ one piece of the next slab's patch in steps 0..HC_PPW-1)
+    load_x(ps, toff, 0);
+    load_w(base, 0);
+    if (tap < HC_PPW && slab + 1 < nslab) {
+#pragma unroll
+      for (int j = 0; j < HC_PPW; ++j)
+        if (j == tap) patch_piece(slab + 1, j);
+    }
+    mma(0, 0);
+    // P2
+    load_w(base, 1);
+    if (more1) stage_w(kt + 1, nb, 0);
+    if (PRE && tap >= 7 && slab + 1 < nslab) relu_pass((slab + 1) & 1, tap - 7);
+    mma(0, 1);
+    // P3
+    load_x(ps, toff, 1);
+    mma(1, 1);
+    // P4: retire everything but this phase's W(t+2) quarter
+    load_w(base, 0);
+    if (more2) {
+      stage_w(kt + 2, cb, 1);
+      hc_wait<2>();
+    } else {
+      hc_wait<0>();
+    }
+    mma(1, 0);
+  }
+  if (!lagging) __builtin_amdgcn_s_barrier();
+  __syncthreads();
+
+  // ---- epilogue: +bias [ReLU] -> fp16 [256 px][256 ch] image in LDS (8-byte units XOR-swizzled by
+  // pixel & 15), then whole 512-B pixel rows + residuals -> global
+  const int mcol = lane & 15, nq = (lane >> 4) * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int col = wn * 64 + i * 16 + nq;
+    const f4 bv = a.bias ? *reinterpret_cast<const f4*>(a.bias + col) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ml = wm * 128 + j * 16 + mcol;
+      f4 v = acc[i][j] + bv;
+      if (a.relu_out) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      typedef float f2v __attribute__((ext_vector_type(2)));
+      const h2 lo = __builtin_convertvector(f2v{v[0], v[1]}, h2);
+      const h2 hi = __builtin_convertvector(f2v{v[2], v[3]}, h2);
+      const int u = (col >> 2) ^ (ml & 15);
+      *reinterpret_cast<uint2*>(&smem[ml * 256 + u * 4]) =
+          make_uint2(__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi));
+    }
+  }
+  __syncthreads();
+  // thread -> 16-B chunk q of pixels row0 + 16 it (it = 0..15): tile row it >> 1, column row0 + 16 (it & 1)
+  const int q = tid & 31, row0 = tid >> 5;
+  const h16* l0 = smem + row0 * 256 + ((2 * q) ^ row0) * 4;
+  const h16* l1 = smem + row0 * 256 + ((2 * q + 1) ^ row0) * 4;
+  const long fbytes = (long)H * W * 512;
+  const long fbase = (long)bt * H * W * 256;
+  auto rsrc = [&](const h16* p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + fbase), (short)0, (int)fbytes, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t ry = rsrc(a.y);
+  auto voff = [&](int it) {
+    const int yy = y0 + (it >> 1), xx = x0 + row0 + 16 * (it & 1);
+    return (yy < H && xx < W) ? (unsigned)(((yy * W + xx) * 256 + q * 8) * 2) : 0x80000000u;
+  };
+  const int nres = (a.res ? 1 : 0) + (a.res2 ? 1 : 0);
+  const h16* r1p = a.res ? a.res : a.res2;
+  const __amdgpu_buffer_rsrc_t rr1 = rsrc(r1p ? r1p : a.y);
+  const __amdgpu_buffer_rsrc_t rr2 = rsrc(a.res2 ? a.res2 : a.y);
+  constexpr int PD = 4;
+  h8 q1[PD], q2[PD];
+  if (nres >= 1) {
+#pragma unroll
+    for (int it = 0; it < PD; ++it) q1[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, voff(it), 0, 0));
+  }
+  if (nres >= 2) {
+#pragma unroll
+    for (int it = 0; it < PD; ++it) q2[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, voff(it), 0, 0));
+  }
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * 16 * 256);
+    const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * 16 * 256);
+    h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+    const unsigned vo = voff(it);
+    if (nres >= 1) {
+      t += q1[it % PD];
+      if (it + PD < 16) q1[it % PD] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, voff(it + PD), 0, 0));
+    }
+    if (nres >= 2) {
+      t += q2[it % PD];
+      if (it + PD < 16) q2[it % PD] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, voff(it + PD), 0, 0));
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vo, 0, 2);
+  }
+}
+
+}  // namespace
+
+int g_hconv_mode = -1;  // vda_debug_hconv: -1 automatic, 0 never, 1 every served shape
+
+// Does the halo kernel serve (and, in automatic mode, win on) this conv?
+bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout) {
+  if (Cout != 256 || Cin % 64 != 0 || Cin <= 0 || g_hconv_mode == 0) return false;
+  if ((long)BT * ((H + HC_TR - 1) / HC_TR) * ((W + HC_TC - 1) / HC_TC) > 0x7fffffffL) return false;
+  if ((long)H * W * Cin >= (1L << 31) || (long)H * W * 512 >= (1L << 31)) return false;
+  if (g_hconv_mode == 1) return true;
+  // measured (tools/bench_hconv.py, 32 frames): 148^2 1.26-1.29x, 74^2 1.07-1.11x, 37^2 0.73-0.76x the
+  // implicit GEMM (a 37^2 map leaves 8 x 32 tiles 23 % empty and too few of them to fill the CUs)
+  return (long)H * W >= 64L * 64L;
+}
+
+int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
+                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st) {
+  if (!vda_conv_hconv_serves(BT, H, W, Cin, Cout)) return 1;
+  HconvArgs a{};
+  a.x = (const h16*)x; a.w = (const h16*)w; a.y = (h16*)y; a.bias = bias;
+  a.res = (const h16*)res; a.res2 = (const h16*)res2;
+  a.H = H; a.W = W; a.Cin = Cin; a.relu_out = relu_out;
+  a.tiles_x = (W + HC_TC - 1) / HC_TC;
+  a.tiles_y = (H + HC_TR - 1) / HC_TR;
+  a.ntiles = BT * a.tiles_x * a.tiles_y;
+  if (pre_relu)
+    hipLaunchKernelGGL(hconv256_kernel<true>, dim3(a.ntiles), dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL(hconv256_kernel<false>, dim3(a.ntiles), dim3(512), 0, st, a);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int vda_debug_hconv(int32_t mode) {
+  g_hconv_mode = mode;
+  return 0;
+}
