@@ -275,6 +275,14 @@ int vda_debug_strip_split(int32_t nsplit);
  */
 int vda_debug_hconv(int32_t mode);
 
+/*
+ * Tuning hook for the depth tail (vda_depth_head): -1 = automatic (the 2-blocks-per-CU depth conv of
+ * csrc/vda_dconv.hip with the resize fused into its patch building), 2 = the same conv on a
+ * materialised resize (bit-identical; needs the workspace), 0 = the older 8-wave halo kernels.  Query
+ * vda_depth_head_workspace after changing it.  Process-global.
+ */
+int vda_debug_dconv(int32_t mode);
+
 #ifdef __cplusplus
 }
 #endif

@@ -316,20 +316,34 @@ def test_c_abi_direct_matches_torch_ops():
     assert rel(yc, ref) < 2e-3 and rel(yn, ref) < 2e-3
 
 
-def test_depth_head_allocates_no_resize_workspace():
-    """The fused depth head never materialises the 518^2 resized map: the op's peak memory is its output
-    plus the inputs (ops.depth_head used to reserve [BT, 518, 518, 128] fp16 per call)."""
+def test_depth_head_workspace_only_when_used():
+    """The op allocates the resized-map workspace exactly when the library's path materialises the
+    resize: the default (resize fused into the depth conv of vda_dconv.hip) none, the materialised
+    variant (vda_debug_dconv(2)) one [BT, 518, 518, C] fp16 map (no unused reservation)."""
     x = h(rnd(2, 296, 296, 128, scale=0.5, seed=76))
     w1 = h(rnd(64, 3, 3, 128, scale=0.03, seed=77))
     b1, w2, b2 = f32(rnd(32, seed=78)), f32(rnd(32, seed=79)), f32(rnd(1, seed=80))
-    torch.cuda.synchronize()
-    base = torch.cuda.memory_allocated()
-    torch.cuda.reset_peak_memory_stats()
-    d = ops.depth_head(x, w1, b1, w2, b2, 518, 518)
-    torch.cuda.synchronize()
-    extra = torch.cuda.max_memory_allocated() - base
-    assert d.shape == (2, 518, 518)
-    assert extra <= 2 * 518 * 518 * 4 + (4 << 20), extra  # the fp32 depth (+ allocator rounding)
+    lib = vda_amd._libvda()
+
+    def extra_bytes():
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated()
+        torch.cuda.reset_peak_memory_stats()
+        d = ops.depth_head(x, w1, b1, w2, b2, 518, 518)
+        torch.cuda.synchronize()
+        assert d.shape == (2, 518, 518)
+        return torch.cuda.max_memory_allocated() - base, d
+
+    dmap = 2 * 518 * 518 * 4
+    extra, d0 = extra_bytes()  # default: resize fused into the depth conv
+    assert extra <= dmap + (4 << 20), extra  # the fp32 depth (+ allocator rounding)
+    lib.vda_debug_dconv(2)
+    try:
+        extra, d1 = extra_bytes()  # materialised resize
+    finally:
+        lib.vda_debug_dconv(-1)
+    assert 2 * 518 * 518 * 128 * 2 <= extra - dmap <= 2 * 518 * 518 * 128 * 2 + (4 << 20), extra
+    assert torch.equal(d0, d1)
 
 
 @pytest.mark.parametrize("Cin,H,W,relu", [(256, 130, 140, False), (128, 129, 131, True)])
@@ -450,8 +464,9 @@ def test_conv3x3_strip_split(Cin, H, W, BT, mode, split):
 @pytest.mark.parametrize("C,Hin,Win,Ho,Wo,BT", [(128, 20, 24, 37, 51, 2), (64, 9, 9, 16, 16, 1), (128, 37, 37, 70, 70, 3),
                                                  (64, 30, 17, 53, 31, 2), (128, 12, 12, 12, 12, 1), (64, 5, 40, 33, 47, 1)])
 def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
-    """Depth tail with the bilinear resize fused into the halo conv's patch staging (the default for
-    C % 64 == 0): bit-identical to the materialised resize + halo conv (vda_debug_force_tile(9)),
+    """Depth tail with the bilinear resize fused into the patch building of the depth conv (default):
+    bit-identical to the materialised resize + the same conv (vda_debug_dconv(2)); and the older
+    fused 8-wave halo conv (vda_debug_dconv(0)) bit-identical to the materialised resize + halo conv (vda_debug_force_tile(9)),
     both interpolating with the same fp32 formula and fp16 rounding; partial tiles, non-square maps,
     identity-size resize, aspect ratios far from 1."""
     x = rnd(BT, C, Hin, Win, seed=145)
@@ -464,14 +479,26 @@ def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
     wn = w1.permute(0, 2, 3, 1)
     split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0).to(DEV).contiguous()
     args = (split, f32(b1), f32(w2.reshape(-1)), f32(b2), Ho, Wo)
-    y = ops.depth_head(xh, *args)
+    y = ops.depth_head(xh, *args)  # default: the 2-blocks-per-CU depth conv, resize fused into its patches
     lib = vda_amd._libvda()
+    lib.vda_debug_dconv(2)  # the same conv on a materialised resize
+    try:
+        y_mat2 = ops.depth_head(xh, *args)
+    finally:
+        lib.vda_debug_dconv(-1)
+    assert torch.equal(y, y_mat2)
+    lib.vda_debug_dconv(0)
+    try:
+        y_fused = ops.depth_head(xh, *args)
+    finally:
+        lib.vda_debug_dconv(-1)
     lib.vda_debug_force_tile(9)
     try:
         y_mat = ops.depth_head(xh, *args)
     finally:
         lib.vda_debug_force_tile(-1)
-    assert torch.equal(y, y_mat)
+    assert torch.equal(y_fused, y_mat)  # the older 8-wave halo kernels, fused vs materialised
+    assert rel(y_fused, ref) < 1e-5
     assert rel(y, ref) < 1e-5
 
 

@@ -8,7 +8,7 @@ for spec in "$@"; do
   D=build/var/$name; mkdir -p $D
   S=${SRC:-vda_depth}
   /opt/rocm/bin/hipcc $FL $defs $EXTRA -c video-depth-anything_amd/csrc/$S.hip -o $D/$S.o
-  objs=$(ls build/*.o | grep -v "/$S.o")
+  objs=$(ls build/*.o | grep -v "/$S.o" | grep -v "/vda_torch.o")
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $objs $D/$S.o -o $D/libvda.so
   echo "built $D ($defs)"
 done

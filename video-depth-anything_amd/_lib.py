@@ -23,7 +23,7 @@ EXPORTED = (
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
     "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_strip_split",
-    "vda_debug_hconv",
+    "vda_debug_hconv", "vda_debug_dconv",
 )
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -88,6 +88,7 @@ def _declare(lib):
         "vda_debug_gemm_desync": ([I], I),
         "vda_debug_strip_split": ([I], I),
         "vda_debug_hconv": ([I], I),
+        "vda_debug_dconv": ([I], I),
     }
     for name, (args, res) in sig.items():
         if name.startswith("vda_debug_") and not hasattr(lib, name):

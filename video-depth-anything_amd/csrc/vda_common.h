@@ -68,6 +68,48 @@ __device__ __forceinline__ h8 bilerp8(h8 a, h8 b, h8 c, h8 d, float wx, float wy
   }
   return o;
 }
+// The same blend with v_fma_mix_f32 reading the fp16 channels straight out of the packed registers
+// (exact f16 -> f32 in the FMA, one rounding): bit-identical to bilerp8 (ux * a as fma(ux, a, -0) keeps
+// the product's sign of zero) in 6 VALU per channel instead of 10 (4 conversions + 6 ops, which
+// -O3 also SLP-packs into v_pk_*_f32, slow beside MFMAs).
+__device__ __forceinline__ float fma_mix_lo(float a, unsigned hb, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(hb), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float fma_mix_hi(float a, unsigned hb, float c) {
+  float d;
+  asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(hb), "v"(c));
+  return d;
+}
+__device__ __forceinline__ float mul_f32(float a, float b) {  // single v_mul_f32 (no SLP packing)
+  float d;
+  asm("v_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ float fma_f32(float a, float b, float c) {
+  float d;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ uint4 bilerp8_mix(uint4 a, uint4 b, uint4 c, uint4 d, float wx, float wy) {
+  const float ux = 1.f - wx, uy = 1.f - wy;
+  const unsigned A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+  const unsigned Cc[4] = {c.x, c.y, c.z, c.w}, D[4] = {d.x, d.y, d.z, d.w};
+  unsigned o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float tl = fma_mix_lo(wx, B[j], fma_mix_lo(ux, A[j], -0.f));
+    const float th = fma_mix_hi(wx, B[j], fma_mix_hi(ux, A[j], -0.f));
+    const float bl = fma_mix_lo(wx, D[j], fma_mix_lo(ux, Cc[j], -0.f));
+    const float bh = fma_mix_hi(wx, D[j], fma_mix_hi(ux, Cc[j], -0.f));
+    const float ol = fma_f32(wy, bl, mul_f32(uy, tl));
+    const float oh = fma_f32(wy, bh, mul_f32(uy, th));
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    o[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{ol, oh}, h2));
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
 __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }

@@ -51,6 +51,13 @@ int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const f
                          float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st);
 int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int Hs, int Ws,
                         int H, int W, int Cin, int Cout, hipStream_t st);
+// depth-tail conv on the resized map, 2 blocks / CU (vda_dconv.hip)
+bool vda_depth_conv_serves(int H, int W, int C);
+int vda_depth_conv(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
+                   int BT, int H, int W, int C, hipStream_t st);
+bool vda_depth_conv_fused_serves(int Hs, int Ws, int H, int W, int C);
+int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
+                         float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st);
 // halo-tiled phased 3x3 conv, Cout = 256 (vda_hconv.hip)
 bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout);
 int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
@@ -1422,7 +1429,22 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
   VDA_CHECK_ARG(C % 8 == 0, "depth head needs C % 8 == 0");
   hipStream_t st = (hipStream_t)stream;
   int rc;
-  // 0) default: resize fused into the halo conv's patch staging (the resized map is never written;
+  // default: the depth conv of vda_dconv.hip (two 4-wave blocks per CU, 64 pixels x all 64 hi/lo rows
+  // per wave) with the bilinear resize fused into its patch building (the resized map is never
+  // written); vda_debug_dconv(2): bilinear resize into ws + the same conv on the materialised map
+  // (bit-identical); vda_debug_dconv(0): the older 8-wave halo kernels below.
+  if (g_force_tile == -1) {
+    rc = vda_depth_conv_fused(x, w1, b1, w2, b2, depth, BT, Hin, Win, Ho, Wo, C, st);
+    if (rc != 1) return rc;
+  }
+  if (g_force_tile == -1 && vda_depth_conv_serves(Ho, Wo, C)) {
+    VDA_CHECK_ARG(ws, "depth head: needs the resize workspace (vda_depth_head_workspace)");
+    rc = vda_upsample_bilinear(x, ws, BT, Hin, Win, C, Ho, Wo, stream);
+    if (rc) return rc;
+    rc = vda_depth_conv(ws, w1, b1, w2, b2, depth, BT, Ho, Wo, C, st);
+    if (rc != 1) return rc;
+  }
+  // 0) resize fused into the halo conv's patch staging (the resized map is never written;
   //    bit-identical to 1 + 2).  vda_debug_force_tile(9) takes the materialised path below.
   if (g_force_tile < 9) {
     rc = vda_depth_halo_fused(x, w1, b1, w2, b2, depth, BT, Hin, Win, Ho, Wo, C, st);
@@ -1474,6 +1496,8 @@ extern "C" int vda_depth_head(const void* x, const void* w1, const float* b1, co
 
 extern "C" int64_t vda_depth_head_workspace(int32_t BT, int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo) {
   if (BT <= 0 || Hin <= 0 || Win <= 0 || C <= 0 || Ho <= 0 || Wo <= 0) return 0;
+  if (g_force_tile == -1 && vda_depth_conv_fused_serves(Hin, Win, Ho, Wo, C)) return 0;  // fused: no resized map
+  if (g_force_tile == -1 && vda_depth_conv_serves(Ho, Wo, C)) return (int64_t)BT * Ho * Wo * C * 2;
   if (g_force_tile < 9 && vda_depth_halo_fused_serves(Hin, Win, Ho, Wo, C)) return 0;  // fused: no resized map
   return (int64_t)BT * Ho * Wo * C * 2;
 }
