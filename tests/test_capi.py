@@ -114,4 +114,5 @@ def test_workspace_queries():
     assert lib.vda_conv2d_workspace(32, 148, 148, 256, 256, 3, 1, 1) == 0   # implicit GEMM: no workspace
     assert lib.vda_conv2d_workspace(32, 37, 37, 1024, 256, 3, 2, 1) == 0    # stride 2: no workspace
     assert lib.vda_depth_head_workspace(32, 296, 296, 128, 518, 518) == 0   # fused resize: none
-    assert lib.vda_depth_head_workspace(2, 20, 20, 32, 518, 518) == 2 * 518 * 518 * 32 * 2  # C % 64: materialised
+    assert lib.vda_depth_head_workspace(2, 20, 20, 32, 518, 518) == 0   # C % 32: fused depth conv
+    assert lib.vda_depth_head_workspace(2, 20, 20, 40, 518, 518) == 2 * 518 * 518 * 40 * 2  # C % 32 != 0: materialised
