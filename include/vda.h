@@ -67,6 +67,18 @@ typedef struct vda_epilogue {
    * an even number of rows (M rounded up to 2).  Row store only, no gamma, activation none/gelu/relu. */
   const float* ln_stats;  /* [round_up(M, 2), 2] or NULL                              */
   const float* ln_colsum; /* [N]                                                     */
+  /* ln_parts > 0: ln_stats instead holds [M, ln_parts, 2] partial (sum, sum of squares) of row m
+   * over ln_parts column blocks (as written through stats_out by the GEMM that produced X); the
+   * epilogue forms mean = sum / K, var = max(sumsq / K - mean^2, 0), rstd = 1 / sqrt(var + ln_eps).
+   * ln_parts <= 4. */
+  int32_t ln_parts;
+  float ln_eps;
+  /* Producer side: write [M, ceil(N / 256), 2] per-row partial (sum, sum of squares) of the fp16
+   * OUTPUT values (after the residual adds) over 256-column blocks, for a following LN-folded GEMM
+   * (ln_parts = ceil(N / 256)): the statistics pass over the row stream is never a separate read.
+   * Row store, no pixel shuffle; computed by a separate partial-sum kernel when the GEMM shape does
+   * not take the phased 256x256 kernel. */
+  float* stats_out;
 } vda_epilogue;
 
 /* Version / diagnostics. */

@@ -597,3 +597,38 @@ def test_conv3x3_hconv_cout256(Cin, H, W, BT, mode):
         lib.vda_debug_force_tile(-1)
         lib.vda_debug_hconv(-1)
     assert rel(y, y2) < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(4001, 1024, 1024), (43840, 1024, 4096), (4001, 384, 1536), (5003, 768, 768),
+                                   (300, 1024, 256), (4001, 1024, 512)])
+def test_gemm_epilogue_row_stats(M, N, K):
+    """proj / fc2 (x += ...) writing per-row partial (sum, sumsq) of their fp16 outputs over 256-column
+    blocks (stats_out; the phased epilogue for the encoder shapes, the separate partial-sum pass for
+    the others), and the next LN-folded GEMM consuming them (ln_parts = P): vs torch sums of the
+    stored values and vs the same fold from vda_row_stats."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 0.5).half().float()
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    r = (torch.randn(M, N, generator=g) * 2 + torch.randn(M, 1, generator=g)).half()
+    P = (N + 255) // 256
+    tok = r.to(DEV).contiguous()
+    st = torch.full((M, P, 2), float("nan"), device=DEV)
+    ops.gemm(h(x), h(w), bias=f32(b), res=tok, out=tok, stats_out=st)
+    y = tok.float().cpu()
+    pad = torch.zeros(M, P * 256)
+    pad[:, :N] = y
+    ref_s = pad.view(M, P, 256).sum(2)
+    ref_q = (pad * pad).view(M, P, 256).sum(2)
+    stc = st.cpu()
+    assert torch.allclose(stc[..., 0], ref_s, rtol=1e-4, atol=1e-3)
+    assert torch.allclose(stc[..., 1], ref_q, rtol=1e-4, atol=1e-3)
+    # consumer: LN fold from the partials vs from vda_row_stats
+    gam, bet = 1 + 0.2 * torch.randn(N, generator=g), 0.1 * torch.randn(N, generator=g)
+    w2 = torch.randn(512, N, generator=g) * N ** -0.5
+    wg = (w2 * gam[None, :]).half()
+    c1, bb = f32(wg.float().sum(1)), f32(w2 @ bet)
+    ya = ops.gemm(tok, wg.to(DEV), bias=bb, ln_stats=st, ln_parts=P, ln_eps=1e-6, ln_colsum=c1)
+    yb = ops.gemm(tok, wg.to(DEV), bias=bb, ln_stats=ops.row_stats(tok, 1e-6), ln_colsum=c1)
+    ref = F.linear(F.layer_norm(y, (N,), gam, bet, eps=1e-6), w2)
+    assert rel(ya, ref) < 2e-3 and rel(ya, yb) < 1e-3

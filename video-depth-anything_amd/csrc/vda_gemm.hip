@@ -58,6 +58,8 @@ int vda_depth_conv(const void* U, const void* w1, const float* b1, const float* 
 bool vda_depth_conv_fused_serves(int Hs, int Ws, int H, int W, int C);
 int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                          float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st);
+// per-row partial statistics of an fp16 matrix (vda_norm.hip): the stats_out fallback
+int vda_row_partials_launch(const void* y, int64_t ldy, float* out, int32_t rows, int32_t N, hipStream_t st);
 // halo-tiled phased 3x3 conv, Cout = 256 (vda_hconv.hip)
 bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout);
 int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
@@ -160,7 +162,19 @@ template <int ACT>
 __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4 v) {
   const vda_epilogue& e = p.epi;
   if (e.ln_stats) {  // LayerNorm folded into the GEMM: rstd * (acc - mean * colsum)
-    const float2 mr = *reinterpret_cast<const float2*>(e.ln_stats + 2L * m);
+    float2 mr;
+    if (e.ln_parts > 0) {  // partial (sum, sumsq) over ln_parts column blocks
+      float sm = 0.f, sq = 0.f;
+      for (int t = 0; t < e.ln_parts; ++t) {
+        const float2 pq = *reinterpret_cast<const float2*>(e.ln_stats + 2L * ((long)m * e.ln_parts + t));
+        sm += pq.x;
+        sq += pq.y;
+      }
+      const float mean = sm / (float)p.K;
+      mr = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq / (float)p.K), 0.f) + e.ln_eps));
+    } else {
+      mr = *reinterpret_cast<const float2*>(e.ln_stats + 2L * m);
+    }
     const f4 c1 = *reinterpret_cast<const f4*>(e.ln_colsum + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = mr.y * fmaf(-mr.x, c1[j], v[j]);
@@ -577,6 +591,55 @@ __global__ __launch_bounds__(NWM * NWN * 64) void gemm_kernel(GemmParams p, int 
   }
 }
 
+// ---- per-row partial statistics in the epilogue (vda_epilogue.stats_out) ----------------------
+// A half-wave (32 lanes) owns one output row per phase-2 iteration, 8 columns per lane.  Each lane
+// accumulates (sum, sum of squares) of its 8 fp16 outputs with v_dot2_f32_f16 for all 16 rows, then
+// one multi-value butterfly over the half-wave leaves lane l with value l of the 32: sum (l & 16 == 0)
+// or sum of squares of row 16 * (l & 15).  Step 1 exchanges whole register pairs with
+// v_permlane16_swap (no selects); steps 2-5 pair lanes i / 15 - i, 7 - i, 3 - i, i ^ 1 by DPP.
+__device__ __forceinline__ void perm16_swap(float& a, float& b) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float halfwave_sum32(float (&v)[32], int lane) {
+  float w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    float a = v[k], b = v[16 + k];
+    perm16_swap(a, b);
+    w[k] = a + b;
+  }
+  const int i = lane & 15;
+  float x[8], y[4], z[2];
+  bool lo = i < 8;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x[k] = (lo ? w[k] : w[k + 8]) + dpp_f<0x140>(lo ? w[k + 8] : w[k]);  // row_mirror
+  lo = (i & 7) < 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) y[k] = (lo ? x[k] : x[k + 4]) + dpp_f<0x141>(lo ? x[k + 4] : x[k]);  // row_half_mirror
+  lo = (i & 3) < 2;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) z[k] = (lo ? y[k] : y[k + 2]) + dpp_f<0x1B>(lo ? y[k + 2] : y[k]);  // quad_perm 3,2,1,0
+  lo = (i & 1) == 0;
+  return (lo ? z[0] : z[1]) + dpp_f<0xB1>(lo ? z[1] : z[0]);  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ void stat_acc(h8 t, float& s, float& q) {
+  const h2 one = h2{(h16)1.f, (h16)1.f};
+  h2 tp[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) tp[k] = h2{t[2 * k], t[2 * k + 1]};
+  s = 0.f;
+  q = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s = __builtin_amdgcn_fdot2(tp[k], one, s, false);
+    q = __builtin_amdgcn_fdot2(tp[k], tp[k], q, false);
+  }
+}
+
 // ---- 256x256 phased kernel -------------------------------------------------------------------
 // 8 waves (2 m x 4 n), wave tile 128 (m) x 64 (n), BK = 64, two K-tile buffers of four 16-KiB
 // half-tile regions [XL | XH | WL | WH].  Every K tile runs as 4 phases; each phase multiplies one
@@ -765,10 +828,16 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     glds16(src, smem + 2 * BUF + wave * 512);
     glds16(src + 8192, smem + 2 * BUF + 4096 + wave * 512);
   }
-  if constexpr (LNF) {  // rows m0 .. m0+255 of [M, 2] fp32 (mean, rstd): 2 pieces of 128 rows, waves 0-1
-    if (wave < 2) {
-      const int r = m0 + wave * 128 + lane * 2;  // this lane's 16 B = rows r, r + 1 (M is even or row r+1 unused)
-      const void* src = r < p.M ? (const void*)(p.epi.ln_stats + (long)r * 2) : (const void*)g_zero_page;
+  if constexpr (LNF) {
+    if (p.epi.ln_parts <= 0) {  // rows m0 .. m0+255 of [M, 2] fp32 (mean, rstd): 2 pieces of 128 rows, waves 0-1
+      if (wave < 2) {
+        const int r = m0 + wave * 128 + lane * 2;  // this lane's 16 B = rows r, r + 1 (M is even or row r+1 unused)
+        const void* src = r < p.M ? (const void*)(p.epi.ln_stats + (long)r * 2) : (const void*)g_zero_page;
+        glds16(src, lnst_lds + wave * 512);
+      }
+    } else if (wave < 2 * p.epi.ln_parts) {  // rows m0 .. m0+255 of [M, P, 2] partial sums: 2P pieces of 1 KiB
+      const long f = (long)m0 * p.epi.ln_parts * 2 + wave * 256 + lane * 4;  // float index of this lane's 16 B
+      const void* src = f < (long)p.M * p.epi.ln_parts * 2 ? (const void*)(p.epi.ln_stats + f) : (const void*)g_zero_page;
       glds16(src, lnst_lds + wave * 512);
     }
   }
@@ -900,9 +969,25 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     if constexpr (LNF) {  // y = rstd * (acc - mean * colsum) + bias (LayerNorm folded, before the activation)
       const float* st = reinterpret_cast<const float*>(lnst_lds);
       const f4* bv = pbv;  // zero when there is no bias
+      const int P = e.ln_parts;
+      const float invK = 1.f / (float)p.K;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float2 mr = *reinterpret_cast<const float2*>(st + 2 * (wm * 128 + j * 16 + mcol));
+        const int rl = wm * 128 + j * 16 + mcol;
+        float2 mr;
+        if (P <= 0) {
+          mr = *reinterpret_cast<const float2*>(st + 2 * rl);
+        } else {  // partial (sum, sumsq) of P column blocks -> (mean, rstd)
+          float sm = 0.f, sq = 0.f;
+          for (int t = 0; t < P; ++t) {
+            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + t));
+            sm += pq.x;
+            sq += pq.y;
+          }
+          const float mean = sm * invK;
+          const float var = fmaxf(fmaf(-mean, mean, sq * invK), 0.f);
+          mr = make_float2(mean, rsqrtf(var + e.ln_eps));
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1089,12 +1174,33 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       phase2(std::integral_constant<int, 0>{});
     } else if (nres == 1) {
       if constexpr (RPF) {
+        if (e.stats_out) {  // + per-row partial (sum, sumsq) of the stored values for a following LN fold
+          static_assert(NIT == 16 && RPI == 16, "stats: a half-wave per row, 16 rows per lane");
+          const bool cval = c < nout;
+          float v[32];
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-          const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
-          const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
-          const h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y)) + rpre[it];
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
+          for (int it = 0; it < NIT; ++it) {
+            const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
+            const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
+            const h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y)) + rpre[it];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
+            stat_acc(cval ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, v[it], v[16 + it]);
+          }
+          const float r = halfwave_sum32(v, lane);
+          const int P = (p.N + 255) / 256;
+          const int m = m0 + row0 + 16 * (lane & 15);
+          const __amdgpu_buffer_rsrc_t rs =
+              __builtin_amdgcn_make_buffer_rsrc((void*)e.stats_out, (short)0, (int)((long)p.M * P * 8), 0x00020000);
+          const unsigned vo = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + ((lane >> 4) & 1)) * 4) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, vo, 0, 0);
+        } else {
+#pragma unroll
+          for (int it = 0; it < NIT; ++it) {
+            const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * RPI * OW);
+            const uint2 hi = *reinterpret_cast<const uint2*>(l1 + it * RPI * OW);
+            const h8 t = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y)) + rpre[it];
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
+          }
         }
       } else {
         phase2(std::integral_constant<int, 1>{});
@@ -1148,7 +1254,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
                                                       int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0) + (LNF ? 1024 : 0)];
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0) + (LNF ? 4096 : 0)];
   const int ntiles = tiles_m * tiles_n;
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
     const uint64_t d = (uint64_t)(((blockIdx.x >> 3) % desync) * stagger_ticks / desync);
@@ -1237,7 +1343,7 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
 }
 
 template <bool CONV, int ACT>
-void launch_act(const GemmParams& p, hipStream_t st) {
+int launch_act(const GemmParams& p, hipStream_t st) {  // returns the tile configuration it launched
   int cfg = g_force_tile;
   if (cfg < 0) {
     // measured on MI355X (tools/bench_gemm.py): 256x256 wins every large-N shape; N = 128 prefers
@@ -1267,17 +1373,26 @@ void launch_act(const GemmParams& p, hipStream_t st) {
     case 5: launch_phased<4, 1, CONV, ACT>(p, st); break;
     default: launch_tile<128, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
   }
+  return cfg;
 }
 
 template <bool CONV>
 int launch(const GemmParams& p, hipStream_t st) {
+  int cfg;
   switch (p.epi.act) {
-    case VDA_ACT_GELU: launch_act<CONV, VDA_ACT_GELU>(p, st); break;
-    case VDA_ACT_GEGLU: launch_act<CONV, VDA_ACT_GEGLU>(p, st); break;
-    case VDA_ACT_RELU: launch_act<CONV, VDA_ACT_RELU>(p, st); break;
-    default: launch_act<CONV, VDA_ACT_NONE>(p, st); break;
+    case VDA_ACT_GELU: cfg = launch_act<CONV, VDA_ACT_GELU>(p, st); break;
+    case VDA_ACT_GEGLU: cfg = launch_act<CONV, VDA_ACT_GEGLU>(p, st); break;
+    case VDA_ACT_RELU: cfg = launch_act<CONV, VDA_ACT_RELU>(p, st); break;
+    default: cfg = launch_act<CONV, VDA_ACT_NONE>(p, st); break;
   }
   VDA_LAUNCH_CHECK();
+  if (p.epi.stats_out) {
+    // the phased 256x256 dense activation-free kernel with exactly one residual writes the partial
+    // row statistics in its epilogue; any other route gets them from a separate partial-sum pass
+    const int nres = (p.epi.res ? 1 : 0) + (p.epi.res2 ? 1 : 0);
+    const bool in_epi = !CONV && cfg == 4 && p.epi.act == VDA_ACT_NONE && !p.epi.rowbias && !p.epi.ln_stats && nres == 1;
+    if (!in_epi) return vda_row_partials_launch(p.y, p.ldy, p.epi.stats_out, p.M, p.N, st);
+  }
   return 0;
 }
 
@@ -1318,6 +1433,8 @@ int check_epi(const vda_epilogue& e, int N) {
   VDA_CHECK_ARG(!e.ln_stats || (e.ln_colsum && e.store == VDA_STORE_ROWS && !e.gamma &&
                                  (e.act == VDA_ACT_NONE || e.act == VDA_ACT_GELU || e.act == VDA_ACT_RELU)),
                 "ln_stats needs ln_colsum, a row store, no gamma, activation none / gelu / relu");
+  VDA_CHECK_ARG(!e.ln_stats || (e.ln_parts >= 0 && e.ln_parts <= 4), "ln_parts must be 0 .. 4");
+  VDA_CHECK_ARG(!e.stats_out || e.store == VDA_STORE_ROWS, "stats_out needs a row store");
   VDA_CHECK_ARG(!e.res || e.ldres % 4 == 0, "ldres % 4");
   VDA_CHECK_ARG(!e.res2 || e.ldres2 % 4 == 0, "ldres2 % 4");
   return 0;
@@ -1384,6 +1501,7 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
   VDA_CHECK_ARG(p.epi.store == VDA_STORE_ROWS && (p.epi.act == VDA_ACT_NONE || p.epi.act == VDA_ACT_RELU),
                 "conv: row store, activation none/relu");
+  VDA_CHECK_ARG(!p.epi.stats_out && !p.epi.ln_stats, "conv: no LayerNorm fold / row statistics");
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
   if (p.up_h > 0) {

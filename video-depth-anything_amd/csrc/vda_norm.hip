@@ -96,6 +96,27 @@ __global__ __launch_bounds__(256) void row_stats_kernel(const h16* __restrict__ 
   if (lane == 0) st[row] = make_float2(mean, rstd);
 }
 
+// Per-row partial (sum, sum of squares) over 256-column blocks of an fp16 matrix: the fallback for
+// vda_epilogue.stats_out when the producing GEMM did not take the phased kernel (which computes them
+// in its epilogue).  One wave per (row, block): 32 lanes x 8 columns.
+__global__ __launch_bounds__(256) void row_partials_kernel(const h16* __restrict__ y, long ldy, float2* __restrict__ st,
+                                                           int rows, int N, int P) {
+  const int lane = threadIdx.x & 63;
+  const long item = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= (long)rows * P) return;
+  const int row = (int)(item / P), blk = (int)(item - (long)row * P);
+  const int c = blk * 256 + (lane & 31) * 8;
+  float s = 0.f, q = 0.f;
+  if (lane < 32 && c < N) {
+    const h8 t = __builtin_bit_cast(h8, ldg16(y + (long)row * ldy + c));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { const float v = (float)t[j]; s += v; q = fmaf(v, v, q); }
+  }
+  s = wave_sum(s);
+  q = wave_sum(q);
+  if (lane == 0) st[item] = make_float2(s, q);
+}
+
 // Narrow rows (C <= 512, the motion modules' C = 256 / 128): one wave would leave lanes idle and
 // wait on one 512-B row, so LPR = C / 8 lanes own a row (one 16-B chunk each) and a wave normalises
 // 64 / LPR rows; the same two-pass statistics, reduced over the row's LPR lanes only.
@@ -315,6 +336,15 @@ extern "C" int vda_row_stats(const void* x, int64_t ldx, float* stats, int32_t r
   VDA_CHECK_ARG(ldx % 8 == 0 && ldx >= C, "ldx must be a multiple of 8 and >= C");
   hipLaunchKernelGGL(row_stats_kernel, dim3((rows + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const h16*)x, (long)ldx,
                      (float2*)stats, rows, C, eps);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+int vda_row_partials_launch(const void* y, int64_t ldy, float* out, int32_t rows, int32_t N, hipStream_t stream) {
+  const int P = (N + 255) / 256;
+  const long items = (long)rows * P;
+  hipLaunchKernelGGL(row_partials_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, stream,
+                     (const h16*)y, (long)ldy, (float2*)out, rows, N, P);
   VDA_LAUNCH_CHECK();
   return 0;
 }

@@ -60,7 +60,8 @@ const void* ptr(OptT t) { return t.has_value() ? t->data_ptr() : nullptr; }
 // vda_epilogue from the optional per-channel / per-row / residual operands (include/vda.h).
 vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma, OptT res,
                       OptT res2, int64_t act, at::ScalarType dt, OptT ln_stats = c10::nullopt,
-                      OptT ln_colsum = c10::nullopt) {
+                      OptT ln_colsum = c10::nullopt, int64_t ln_parts = 0, double ln_eps = 1e-6,
+                      OptT stats_out = c10::nullopt) {
   vda_epilogue e;
   std::memset(&e, 0, sizeof(e));
   if (bias) need_contig(*bias, at::kFloat, "bias", x);
@@ -89,17 +90,30 @@ vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, in
     TORCH_CHECK(ln_colsum.has_value(), "vda gemm: ln_stats needs ln_colsum");
     need_contig(*ln_stats, at::kFloat, "ln_stats", x);
     need_contig(*ln_colsum, at::kFloat, "ln_colsum", x);
-    TORCH_CHECK(ln_stats->dim() == 2 && ln_stats->size(1) == 2 && ln_stats->size(0) >= (x.size(0) + 1) / 2 * 2,
-                "vda gemm: ln_stats must be [round_up(M, 2), 2] (from vda.row_stats)");
+    if (ln_parts > 0) {
+      TORCH_CHECK(ln_parts <= 4 && ln_stats->dim() == 3 && ln_stats->size(0) >= x.size(0) &&
+                      ln_stats->size(1) == ln_parts && ln_stats->size(2) == 2,
+                  "vda gemm: with ln_parts = P, ln_stats must be [M, P, 2] partial sums (a GEMM's stats_out), P <= 4");
+    } else {
+      TORCH_CHECK(ln_stats->dim() == 2 && ln_stats->size(1) == 2 && ln_stats->size(0) >= (x.size(0) + 1) / 2 * 2,
+                  "vda gemm: ln_stats must be [round_up(M, 2), 2] (from vda.row_stats)");
+    }
     e.ln_stats = (const float*)ln_stats->data_ptr();
     e.ln_colsum = (const float*)ln_colsum->data_ptr();
+    e.ln_parts = (int32_t)ln_parts;
+    e.ln_eps = (float)ln_eps;
+  }
+  if (stats_out) {
+    need_contig(*stats_out, at::kFloat, "stats_out", x);
+    e.stats_out = (float*)stats_out->data_ptr();
   }
   return e;
 }
 
 // ---- linear / 1x1 conv / ConvTranspose(k=s) ------------------------------------------------------
 Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, Tensor out) {
+                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
+                 OptT stats_out, Tensor out) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "vda gemm: x must be a 2-D row-major (possibly row-strided) matrix");
   need_contig(w, dt, "w", x);
@@ -109,9 +123,14 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
   TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == nout && out.stride(1) == 1 &&
                   out.scalar_type() == dt && out.device() == x.device(),
               "vda gemm: out must be [", M, ", ", nout, "] ", dt, " with unit column stride");
+  if (stats_out)
+    TORCH_CHECK(stats_out->dim() == 3 && stats_out->size(0) >= M && stats_out->size(1) == (nout + 255) / 256 &&
+                    stats_out->size(2) == 2 && stats_out->scalar_type() == at::kFloat && stats_out->is_contiguous(),
+                "vda gemm: stats_out must be a contiguous float [M, ceil(N / 256), 2]");
   if (x.is_meta()) return out;
   const at::OptionalDeviceGuard g(x.device());
-  vda_epilogue e = make_epi(x, bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt, ln_stats, ln_colsum);
+  vda_epilogue e = make_epi(x, bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt, ln_stats, ln_colsum, ln_parts,
+                            ln_eps, stats_out);
   const int rc = dt == at::kHalf
                      ? vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), (int32_t)M,
                                 (int32_t)N, (int32_t)K, &e, stream_of(x))
@@ -123,17 +142,21 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
 }
 
 Tensor gemm(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-            OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum) {
+            OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
+            OptT stats_out) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "vda gemm: x and w must be 2-D");
   const int64_t nout = act == VDA_ACT_GEGLU ? w.size(0) / 2 : w.size(0);
   Tensor out = at::empty({x.size(0), nout}, x.options().dtype(dt));
-  return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, out);
+  return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps,
+                   stats_out, out);
 }
 
 Tensor& gemm_out(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
-                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, Tensor& out) {
-  gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, out);
+                 OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
+                 OptT stats_out, Tensor& out) {
+  gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps, stats_out,
+            out);
   return out;
 }
 
@@ -405,10 +428,11 @@ Tensor depth_resize(const Tensor& depth, int64_t ho, int64_t wo) {
 TORCH_LIBRARY(vda, m) {
   m.def("gemm(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
-        "Tensor? ln_colsum=None) -> Tensor");
+        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None) -> Tensor");
   m.def("gemm.out(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
-        "Tensor? ln_colsum=None, *, Tensor(a!) out) -> Tensor(a!)");
+        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, *, "
+        "Tensor(a!) out) -> Tensor(a!)");
   m.def("row_stats(Tensor x, float eps) -> Tensor");
   m.def("conv_transpose_ks(Tensor x, Tensor w, Tensor bias, int BT, int h, int w_, int k) -> Tensor");
   m.def("conv2d(Tensor x, Tensor w, int ks=3, int stride=1, int pad=1, Tensor? bias=None, bool pre_relu=False, "

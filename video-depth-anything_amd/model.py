@@ -492,21 +492,40 @@ class VideoDepthAnything(nn.Module):
         taps = self.intermediate_layer_idx[self.encoder]
         feats: List[torch.Tensor] = []
         cls: Optional[List[torch.Tensor]] = [] if self.use_clstoken else None
+        # LN statistics: block 0's norm1 from a row-statistics pass over the patch tokens; every later
+        # norm1 / norm2 from the per-row partial sums the proj / fc2 GEMM epilogues write while they
+        # update the residual stream (stats_out), so no LayerNorm reads the 90-MB token matrix again
+        C = P.C
+        nparts = (C + 255) // 256
+        epistats = P.lnfold and nparts <= 4 and os.environ.get("VDA_NO_EPISTATS", "0") != "1"
+        if epistats:
+            st_a = torch.empty(tok.shape[0], nparts, 2, device=tok.device, dtype=torch.float32)
+            st_b = torch.empty_like(st_a)
+        stats, parts = None, 0
         for i, q in enumerate(P.blocks):
-            if P.lnfold:  # norm1 folded into the qkv GEMM (statistics only: 8 bytes per token)
-                qkv = ops.gemm(tok, q.qkv_w, bias=q.qkv_b, ln_stats=ops.row_stats(tok, 1e-6), ln_colsum=q.qkv_c1)
+            if P.lnfold:  # norm1 folded into the qkv GEMM (statistics only)
+                if stats is None:
+                    stats, parts = ops.row_stats(tok, 1e-6), 0
+                qkv = ops.gemm(tok, q.qkv_w, bias=q.qkv_b, ln_stats=stats, ln_parts=parts, ln_eps=1e-6,
+                               ln_colsum=q.qkv_c1)
             else:
                 qkv = ops.gemm(ops.layernorm(tok, q.n1w, q.n1b, 1e-6), q.qkv_w, bias=q.qkv_b)
             at = ops.spatial_attention(qkv, BT, ntok, P.heads, 64)
             del qkv
-            ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok)
+            ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok, stats_out=st_a if epistats else None)
             if P.lnfold:  # norm2 folded into the fc1 GEMM
-                f = ops.gemm(tok, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, ln_stats=ops.row_stats(tok, 1e-6),
+                if epistats:
+                    stats, parts = st_a, nparts
+                else:
+                    stats, parts = ops.row_stats(tok, 1e-6), 0
+                f = ops.gemm(tok, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, ln_stats=stats, ln_parts=parts, ln_eps=1e-6,
                              ln_colsum=q.fc1_c1, tag="enc_fc1")
             else:
                 f = ops.gemm(ops.layernorm(tok, q.n2w, q.n2b, 1e-6), q.fc1_w, bias=q.fc1_b, act=ACT_GELU,
                              tag="enc_fc1")
-            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok)
+            last = i + 1 == len(P.blocks)
+            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok, stats_out=st_b if epistats and not last else None)
+            stats, parts = (st_b, nparts) if epistats else (None, 0)
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
                 feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
