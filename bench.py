@@ -295,12 +295,12 @@ def roofline(model, launches):
     f1 = pmc("pmc_fc1") or {}
     mfma_busy = None
     for name, e in (pmc("pmc_mfma") or {}).get("kernels", {}).items():
-        if "gemm256_kernel<2, 2, false, 1, false>" in name:
+        if "gemm256_kernel<2, 2, false, 1, false, true>" in name:  # fc1: dense, GELU, LayerNorm folded
             mfma_busy = e.get("mfma_busy")
     return {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": f1.get("hbm_bytes_per_launch"),
             "mfma_busy_pmc": mfma_busy,
-            "kernel": f"gemm256_kernel<2,2,dense,GELU> (encoder fc1) M={M} N={4 * C} K={C}",
+            "kernel": f"gemm256_kernel<2,2,dense,GELU,LN-fold> (encoder norm2 + fc1) M={M} N={4 * C} K={C}",
             "flop_per_launch": flop, "avg_launch_ms": round(ms, 4), "launches": len(rec)}
 
 
