@@ -409,6 +409,8 @@ __device__ __forceinline__ void rope_frag(h8& q, h8& k, int t, int c0, int C, fl
   }
 }
 
+__device__ __attribute__((aligned(64))) uint4 g_ta_zero[4];
+
 #ifndef VDA_TA_NW
 #define VDA_TA_NW 4  // waves (heads of one site) per temporal-attention block
 #endif
@@ -512,6 +514,124 @@ __global__ __launch_bounds__(64 * VDA_TA_NW) void temporal_attn_kernel(const h16
   }
 }
 
+// Temporal attention with the (site, head)'s q, k and v rows staged in LDS (north_star; verdict r1
+// item 10).  The direct-load kernel above reads its K / Q fragments as 32-B pieces of 32 different
+// frame rows per instruction (rows S * 3C apart), which held it at ~3.5 TB/s.  Here each wave moves
+// its head's three 32 x D tiles into LDS with global_load_lds, 16 B per lane, whole D*2-B row
+// segments per 16 / 4 / 2 lanes (D = 128 / 64 / 32), then reads the MFMA fragments from LDS.  LDS
+// image: row r of a tile = D halfs, 16-B chunk c at position c ^ ((r / (16 / CH)) & (CH - 1)),
+// CH = D / 8: conflict-free for the K / Q fragment reads (ds_read_b128 lane groups = 16 rows of one
+// chunk).  The output goes back through the q tile so it is stored as whole row segments too.
+// Waves never share LDS, so the only sync is each wave's own vmcnt + one block barrier.
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW) void temporal_attn_lds_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                                  int B, int T, int S, int H, float scale_log2,
+                                                                  float rope_theta) {
+  constexpr int CH = D / 8;                 // 16-B chunks per row
+  constexpr int RPG = 16 / CH;              // rows per 256-B bank line
+  constexpr int TILE = 32 * D;              // halfs per tensor tile
+  constexpr int NI = 32 * CH / 64;          // DMA instructions per tensor
+  constexpr int NST = D / 16;
+  constexpr int NDT = D / 32;
+  __shared__ __attribute__((aligned(16))) h16 sm[NW * 3 * TILE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long item = (long)blockIdx.x * NW + wave;
+  const long nitems = (long)B * S * H;
+  const bool active = item < nitems;
+  const int hh = active ? (int)(item % H) : 0;
+  const long bs = active ? item / H : 0;
+  const int s = (int)(bs % S), b = (int)(bs / S);
+  const int C = H * D;
+  const long ld = 3L * C;
+  h16* tq = sm + wave * 3 * TILE;
+  h16* tk = tq + TILE;
+  h16* tv = tk + TILE;
+  auto pos = [](int row, int c) { return c ^ ((row / RPG) & (CH - 1)); };
+
+  // stage q, k, v: slot sl = i * 64 + lane of a tile holds row sl / CH, chunk pos(row, sl % CH)
+#pragma unroll
+  for (int z = 0; z < 3; ++z) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int sl = i * 64 + lane;
+      const int row = sl / CH;
+      const int c = pos(row, sl % CH);
+      const void* src = g_ta_zero;
+      if (active && row < T) src = qkv + ((long)(b * T + row) * S + s) * ld + z * C + hh * D + c * 8;
+      __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)(tq + z * TILE + i * 512), 16, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // Sᵀ = K Qᵀ: lane (r32, hf) holds K / Q row r32, channels st * 16 + hf * 8 .. + 7
+  const int r32 = lane & 31, hf = lane >> 5;
+  f16x acc = {};
+#pragma unroll
+  for (int st = 0; st < NST; ++st) {
+    const int c = st * 2 + hf;
+    h8 kf = *reinterpret_cast<const h8*>(tk + r32 * D + pos(r32, c) * 8);
+    h8 qf = *reinterpret_cast<const h8*>(tq + r32 * D + pos(r32, c) * 8);
+    if (rope_theta > 0.f) rope_frag(qf, kf, r32, hh * D + c * 8, C, rope_theta);
+    acc = mfma32(kf, qf, acc);
+  }
+  // softmax over keys (lane holds keys (r&3)+8(r>>2)+4hf for query r32; partner lane^32 the rest);
+  // rows >= T are zero in LDS and masked here
+  float mx = -INFINITY;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    float t = acc[r] * scale_log2;
+    if (key >= T) t = -INFINITY;
+    acc[r] = t;
+    mx = fmaxf(mx, t);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+  h8 pf[2];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float p = exp2f(acc[r] - mx);
+    sum += p;
+    pf[r >> 3][r & 7] = (h16)p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+
+  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    f16x o = {};
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      // tr16 read: group grp -> key rows 16st + 4*(grp>>1) + q4 (+8), cols dt*32 + (grp&1)*16 + 4p4
+      const int col = dt * 32 + (grp & 1) * 16 + 4 * p4;
+      const int r0 = 16 * st + 4 * (grp >> 1) + q4;
+      const h4 v0 = lds_read_tr16(tv + r0 * D + pos(r0, col >> 3) * 8 + (col & 7));
+      const h4 v1 = lds_read_tr16(tv + (r0 + 8) * D + pos(r0 + 8, col >> 3) * 8 + (col & 7));
+      const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+      o = mfma32(vf, pf[st], o);
+    }
+    // lane holds Oᵀ[d = dt*32 + (r&3) + 8(r>>2) + 4hf][q = r32]: into the q tile (its fragments are
+    // consumed) as rows, so the stores below write whole D*2-B row segments
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const int d = dt * 32 + 8 * gq + 4 * hf;
+      h4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = (h16)(o[gq * 4 + r] * inv);
+      *reinterpret_cast<h4*>(tq + r32 * D + pos(r32, d >> 3) * 8 + (d & 7)) = v;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int sl = i * 64 + lane;
+    const int row = sl / CH, c = sl % CH;
+    const uint4 v = *reinterpret_cast<const uint4*>(tq + row * D + pos(row, c) * 8);
+    if (active && row < T) *reinterpret_cast<uint4*>(out + ((long)(b * T + row) * S + s) * C + hh * D + c * 8) = v;
+  }
+}
+
 }  // namespace
 
 extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int32_t N, int32_t H,
@@ -545,6 +665,26 @@ extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int
   dim3 grid((unsigned)((items + VDA_TA_NW - 1) / VDA_TA_NW));
   hipStream_t st = (hipStream_t)stream;
   const float sl = scale * 1.4426950408889634f;
+  // q / k / v rows staged in LDS for the head dims the model uses (128 at C = 1024, 32 at C = 256, 8
+  // heads); VDA_TA_OLD selects the direct-load kernel (A/B only)
+  static const bool ta_old = getenv("VDA_TA_OLD") != nullptr;
+  if (!ta_old && (D == 32 || D == 64 || D == 128)) {
+    const int nw = D == 128 ? 2 : 4;  // 24 / 12 / 6 KiB of LDS per wave
+    if (H % nw == 0) {
+      const unsigned g = (unsigned)((items + nw - 1) / nw);
+      if (D == 128)
+        hipLaunchKernelGGL((temporal_attn_lds_kernel<128, 2>), dim3(g), dim3(128), 0, st, (const h16*)qkv, (h16*)out, B, T,
+                           S, H, sl, rope_theta);
+      else if (D == 64)
+        hipLaunchKernelGGL((temporal_attn_lds_kernel<64, 4>), dim3(g), dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T,
+                           S, H, sl, rope_theta);
+      else
+        hipLaunchKernelGGL((temporal_attn_lds_kernel<32, 4>), dim3(g), dim3(256), 0, st, (const h16*)qkv, (h16*)out, B, T,
+                           S, H, sl, rope_theta);
+      VDA_LAUNCH_CHECK();
+      return 0;
+    }
+  }
   const int dp = (D + 15) / 16 * 16;
 #define VDA_TA(DPV) hipLaunchKernelGGL(temporal_attn_kernel<DPV>, grid, dim3(64 * VDA_TA_NW), 0, st, (const h16*)qkv, (h16*)out, B, T, S, H, D, sl, rope_theta)
   switch (dp) {
