@@ -83,6 +83,8 @@ typedef struct vda_epilogue {
 
 /* Version / diagnostics. */
 const char* vda_version(void);
+/* sizeof(vda_epilogue) as compiled into the library (bindings check their mirror against it). */
+int64_t vda_epilogue_size(void);
 const char* vda_last_error(void);
 
 /*

@@ -16,7 +16,7 @@ TORCH_LIB_PATH = os.path.join(_HERE, "libvda_torch.so")  # TORCH_LIBRARY(vda) ov
 
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
-    "vda_version", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
+    "vda_version", "vda_epilogue_size", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
     "vda_row_stats", "vda_groupnorm", "vda_groupnorm_workspace",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
@@ -45,7 +45,8 @@ class Epilogue(ctypes.Structure):
         ("gamma", c_void_p), ("res", c_void_p), ("ldres", c_int64), ("res2", c_void_p),
         ("ldres2", c_int64), ("act", c_int32), ("store", c_int32), ("ps_k", c_int32),
         ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
-        ("ln_stats", c_void_p), ("ln_colsum", c_void_p),
+        ("ln_stats", c_void_p), ("ln_colsum", c_void_p), ("ln_parts", c_int32), ("ln_eps", c_float),
+        ("stats_out", c_void_p),
     ]
 
 
@@ -58,6 +59,7 @@ def _declare(lib):
     EP = POINTER(Epilogue)
     sig = {
         "vda_version": ([], ctypes.c_char_p),
+        "vda_epilogue_size": ([], L),
         "vda_last_error": ([], ctypes.c_char_p),
         "vda_gemm": ([P, L, P, P, L, I, I, I, EP, P], I),
         "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P, L, P], I),
@@ -111,6 +113,9 @@ def lib():
     try:
         l = ctypes.CDLL(LIB_PATH)
         _declare(l)
+        if l.vda_epilogue_size() != ctypes.sizeof(Epilogue):  # the ctypes mirror must match include/vda.h
+            raise OSError(f"vda_epilogue is {l.vda_epilogue_size()} bytes in the library, {ctypes.sizeof(Epilogue)} "
+                          f"in _lib.Epilogue: rebuild libvda.so or update the mirror")
         sched = os.environ.get("VDA_GEMM_SCHED")  # tuning: "persist_blocks,stagger_ticks"
         if sched and hasattr(l, "vda_debug_gemm_sched"):
             pb, st = (int(v) for v in sched.split(","))

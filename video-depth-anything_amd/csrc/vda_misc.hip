@@ -13,7 +13,8 @@ int vda_set_error(int code, const char* msg) {
   return code;
 }
 
-extern "C" const char* vda_version(void) { return "libvda 0.1 (gfx950, fp16 MFMA)"; }
+extern "C" const char* vda_version(void) { return "libvda 0.2 (gfx950, fp16 MFMA)"; }
+extern "C" int64_t vda_epilogue_size(void) { return (int64_t)sizeof(vda_epilogue); }
 extern "C" const char* vda_last_error(void) { return g_err; }
 
 // upsample tuning (A/B builds): outputs per thread, non-temporal output stores.  Measured
