@@ -24,8 +24,7 @@ def probe(M, N, K, act, sched=(-1, 0)):
     med = np.median(d, axis=0)
     print(f"{M}x{N}x{K} act{act} sched{sched}: blocks {len(v)}  start spread {v[:,0].max()-v[:,0].min():.1f}us  "
           + "  ".join(f"{n}={m:.2f}" for n, m in zip(names, med)) + f"  tile={np.median(v[:,7]-v[:,0]):.2f}", flush=True)
-probe(43840, 3072, 64, 0)
 probe(43840, 3072, 1024, 0)
 probe(43840, 4096, 1024, ACT_GELU)
 probe(43840, 1024, 4096, 0)
-probe(43840, 3072, 1024, 0, (0, 0))
+probe(43840, 1024, 1024, 0)

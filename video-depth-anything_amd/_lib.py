@@ -13,6 +13,10 @@ from ctypes import c_float, c_int32, c_int64, c_void_p, POINTER
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VDA_LIB_OVERRIDE") or os.path.join(_HERE, "libvda.so")  # override: tuning experiments only
 TORCH_LIB_PATH = os.path.join(_HERE, "libvda_torch.so")  # TORCH_LIBRARY(vda) over the C ABI (csrc/vda_torch.cpp)
+if os.environ.get("VDA_LIB_OVERRIDE"):  # tuning builds: the op library linked next to the override libvda.so
+    _ov = os.path.join(os.path.dirname(os.path.abspath(os.environ["VDA_LIB_OVERRIDE"])), "libvda_torch.so")
+    if os.path.exists(_ov):
+        TORCH_LIB_PATH = _ov
 
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
