@@ -384,15 +384,29 @@ __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int t
   tn = in_group / gsize;
 }
 
-// gelu(x) = x * Phi(x), Phi linearly interpolated from the LDS copy of phi_table.h (1/128 steps on
-// [-8, 8], clamped outside): |error| <= 2.2e-6 absolute, far below the fp16 output rounding, for
-// about half the issue cycles of the erf form (which needs a v_rcp and a v_exp per element).
-__device__ __forceinline__ float gelu_tab(float x, const float* tab) {
-  const float u = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, 1024.f), 0.f, 2047.9998f);  // < 2048: i <= 2047
-  const int i = (int)u;
-  const float t = __builtin_amdgcn_fractf(u);
-  const float2 ab = *reinterpret_cast<const float2*>(tab + 2 * i);
-  return x * fmaf(t, ab.y, ab.x);
+// gelu(x) = x * Phi(x), Phi from the LDS copy of phi_table.h: 2,048 lines A_i + B_i x, one per
+// 1/128-wide interval centred on x_i = -8 + i/128 (clamped outside [-8, 8]), |error| <= 1.3e-6
+// absolute, far below the fp16 output rounding.  The interval is picked by the magic add
+// v = x*128 + (1.5*2^23 + 1024), whose low mantissa bits are round(x*128) + 1024; its byte offset
+// (bits << 3, wrapping the exponent bits away) feeds one 8-byte LDS read of {A_i, B_i}, so a value
+// costs fma + med3 + shift-add + fma + mul (the erf form needs a v_rcp and a v_exp per element;
+// round 1's interpolating table needed a cvt and a fract more).
+constexpr float PHI_MAGIC = 12583936.f;                        // 1.5 * 2^23 + 1024
+constexpr float PHI_LO = 12582912.f, PHI_HI = 12584959.f;      // node 0 and node 2047
+constexpr unsigned PHI_BIAS = 0x4B400000u << 3;                // bits(1.5 * 2^23) * 8 (mod 2^32)
+constexpr int PHI_LDS_HALVES = 8192;                           // 16 KiB of LDS
+typedef float phi_f2 __attribute__((ext_vector_type(2)));
+typedef VDA_LDS const phi_f2* lds_cf2p;
+__device__ __forceinline__ unsigned phi_base(const float* tab) {
+  return (unsigned)(uintptr_t)(VDA_LDS const float*)tab - PHI_BIAS;
+}
+__device__ __forceinline__ phi_f2 phi_line(float x, unsigned phib) {
+  const float v = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, PHI_MAGIC), PHI_LO, PHI_HI);
+  return *(lds_cf2p)(uintptr_t)((__builtin_bit_cast(unsigned, v) << 3) + phib);
+}
+__device__ __forceinline__ float gelu_tab(float x, unsigned phib) {
+  const phi_f2 ab = phi_line(x, phib);
+  return x * fmaf(x, ab.y, ab.x);
 }
 
 __device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
@@ -667,7 +681,8 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   // GELU / GEGLU epilogues read Phi from a 16-KiB LDS table (phi_table.h) staged in the prologue
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
   const float* phi_lds = reinterpret_cast<const float*>(smem + 2 * BUF);
-  h16* lnst_lds = smem + 2 * BUF + (TAB ? 8192 : 0);  // LNF: [256][2] fp32 (mean, rstd)
+  const unsigned phib = phi_base(phi_lds);
+  h16* lnst_lds = smem + 2 * BUF + (TAB ? PHI_LDS_HALVES : 0);  // LNF: [256][2] fp32 (mean, rstd)
 
   // thread id laundered through a volatile move: every lane-derived address below is recomputed
   // per tile instead of being hoisted out of the persistent tile loop (and spilled across it)
@@ -1036,19 +1051,14 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 8; j += 4) {
-          float t[16];
-          int ix[16];
+          phi_f2 ab[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) ab[k] = phi_line(acc[i][j + k / 4][k % 4], phib);
 #pragma unroll
           for (int k = 0; k < 16; ++k) {
-            const float u = __builtin_amdgcn_fmed3f(fmaf(acc[i][j + k / 4][k % 4], 128.f, 1024.f), 0.f, 2047.9998f);
-            ix[k] = (int)u;
-            t[k] = __builtin_amdgcn_fractf(u);
+            const float a = acc[i][j + k / 4][k % 4];
+            acc[i][j + k / 4][k % 4] = a * fmaf(a, ab[k].y, ab[k].x);
           }
-          float2 ab[16];
-#pragma unroll
-          for (int k = 0; k < 16; ++k) ab[k] = *reinterpret_cast<const float2*>(phi_lds + 2 * ix[k]);
-#pragma unroll
-          for (int k = 0; k < 16; ++k) acc[i][j + k / 4][k % 4] *= fmaf(t[k], ab[k].y, ab[k].x);
         }
     }
     auto phase1 = [&](auto g_tag) {
@@ -1069,7 +1079,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           if constexpr (ACT == VDA_ACT_GEGLU) {
             const f4 vh = acc[i][j], vg = acc[i + 1][j];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phi_lds) : gelu_erf(vg[r]));
+            for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phib) : gelu_erf(vg[r]));
             col = ((wn * 64 + i * 16) >> 1) + nq;
           } else {
             v = acc[i][j];
@@ -1254,7 +1264,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
                                                       int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? 8192 : 0) + (LNF ? 4096 : 0)];
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0)];
   const int ntiles = tiles_m * tiles_n;
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
     const uint64_t d = (uint64_t)(((blockIdx.x >> 3) % desync) * stagger_ticks / desync);
