@@ -62,6 +62,9 @@ def parse():
                     help="frames of the CPU-oracle clip timed as the cpu_baseline (0 disables)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-launch event probe")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a captured HIP graph")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="clips in flight per GPU: step i runs on HIP stream i %% streams (the fc1 roofline "
+                         "probe then runs in a single-stream pass after the timed region)")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the per-step depth gather to rank 0")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsal)")
     ap.add_argument("--dry-run", action="store_true",
@@ -185,7 +188,19 @@ def main():
     pending = []  # async gathers in flight (two steps deep)
     gbufs = ([[None] * world for _ in range(2)]) if gather else None
 
+    strs = []
+    if args.streams > 1 and dev.type == "cuda":
+        strs = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
+        for st in strs:
+            st.wait_stream(torch.cuda.current_stream(dev))
+
     def step(i):
+        if strs:
+            with torch.cuda.stream(strs[i % len(strs)]):
+                return step1(i)
+        return step1(i)
+
+    def step1(i):
         d = model(x)
         if gather:
             # clip-parallel output path: every step's depth goes to rank 0 (RCCL gather on the
@@ -223,7 +238,8 @@ def main():
     if dist:
         tdist.barrier()
     probe = not args.no_probe and not args.graph
-    if probe:
+    live = probe and not strs  # concurrent clips share the CUs: per-launch durations would not be the kernel's
+    if live:
         ops.enable_probe(["enc_fc1"])
     sync()
     t0 = time.perf_counter()
@@ -235,7 +251,7 @@ def main():
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
-    launches = ops.take_probe() if probe else {}
+    launches = ops.take_probe() if live else {}
     elapsed = max_over_ranks(elapsed, dev, tdist, args.backend)
     frames = world * args.steps * args.clips_per_gpu * T
     value = frames / elapsed
@@ -245,8 +261,20 @@ def main():
         got = gbufs[(args.steps - 1) % 2]
         if not all(bool(torch.isfinite(t).all()) for t in got):
             raise RuntimeError("non-finite gathered depth")
+    probe_steps = 0
+    if probe and not live:  # the same forward, one clip at a time, after the timed region
+        probe_steps = min(args.steps, 10)
+        ops.enable_probe(["enc_fc1"])
+        for _ in range(probe_steps):
+            model(x)
+        sync()
+        launches = ops.take_probe()
 
     roof = roofline(model, launches)
+    if roof:
+        roof["probe"] = ("HIP events on the launch stream over the timed region" if live else
+                         f"HIP events on the launch stream over {probe_steps} single-stream forwards after the "
+                         f"timed region ({len(strs)} clips in flight would share the CUs)")
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline_frames > 0:
         cpu = cpu_baseline(model, x, enc, args.cpu_baseline_frames, H, W)
@@ -264,7 +292,8 @@ def main():
             "config": {"workload": f"VideoDepthAnything.forward {enc} {args.clips_per_gpu}x{T}x3x{H}x{W} per GPU",
                        "encoder": enc, "frames_per_clip": T, "H": H, "W": W,
                        "clips_per_gpu": args.clips_per_gpu, "parallelism": f"clip-parallel dp{world}",
-                       "ranks": world, "depth_gather_to_rank0": bool(gather), "hip_graph": bool(args.graph)},
+                       "ranks": world, "depth_gather_to_rank0": bool(gather), "hip_graph": bool(args.graph),
+                       "clips_in_flight": max(1, args.streams)},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if gflop:

@@ -20,6 +20,7 @@ Preprocessing (bicubic resize + normalise) and the final depth resize run as lib
 """
 from __future__ import annotations
 
+import contextlib
 import math
 from typing import Callable, List, Optional, Sequence
 
@@ -125,61 +126,99 @@ def interpolate_frames(pre: Sequence[np.ndarray], post: Sequence[np.ndarray]) ->
     return [pre[i] * (1 - w[i]) + post[i] * w[i] for i in range(n)]
 
 
-def stitch(depth_list: List[np.ndarray], n_frames: int) -> np.ndarray:
-    """depth_list: per-window depth frames concatenated (32 per window) -> [n_frames, h, w]."""
-    aligned: List[np.ndarray] = []
-    ref_align: List[np.ndarray] = []
-    align_len = OVERLAP - INTERP_LEN
-    kf_align = KEYFRAMES[:align_len]
-    for fid in range(0, len(depth_list), INFER_LEN):
-        if not aligned:
-            aligned += depth_list[:INFER_LEN]
+class Stitcher:
+    """The reference's stitch loop (video_depth.py:379-413) taken one window at a time, so the host
+    aligns window k while the GPU computes window k + 1.  ``add`` takes the windows in order.  Only
+    the last INTERP_LEN aligned frames can still change (the next window blends into them), so every
+    earlier one is written straight into the preallocated [n_frames, h, w] result as it settles."""
+
+    def __init__(self, n_frames: int):
+        self.n = int(n_frames)
+        self.out: Optional[np.ndarray] = None
+        self.done = 0
+        self.aligned: List[np.ndarray] = []
+        self.ref_align: List[np.ndarray] = []
+
+    def _flush(self, keep: int):
+        if self.out is None:
+            self.out = np.empty((self.n,) + self.aligned[0].shape, dtype=self.aligned[0].dtype)
+        while len(self.aligned) > keep and self.done < self.n:
+            self.out[self.done] = self.aligned.pop(0)
+            self.done += 1
+
+    def add(self, win: Sequence[np.ndarray]):
+        align_len = OVERLAP - INTERP_LEN
+        kf_align = KEYFRAMES[:align_len]
+        if not self.aligned:
+            self.aligned += list(win[:INFER_LEN])
             for kf in kf_align:
-                ref_align.append(depth_list[fid + kf])
-            continue
-        cur = [depth_list[fid + i] for i in range(len(kf_align))]
-        scale, shift = compute_scale_and_shift(np.concatenate(cur), np.concatenate(ref_align),
-                                               np.concatenate(np.ones_like(ref_align) == 1))
-        pre = aligned[-INTERP_LEN:]
-        post = list(depth_list[fid + align_len: fid + OVERLAP])
+                self.ref_align.append(win[kf])
+            self._flush(INTERP_LEN)
+            return
+        cur = [win[i] for i in range(len(kf_align))]
+        scale, shift = compute_scale_and_shift(np.concatenate(cur), np.concatenate(self.ref_align),
+                                               np.concatenate(np.ones_like(self.ref_align) == 1))
+        pre = self.aligned[-INTERP_LEN:]
+        post = list(win[align_len:OVERLAP])
         for i in range(len(post)):
             post[i] = post[i] * scale + shift
             post[i][post[i] < 0] = 0
-        aligned[-INTERP_LEN:] = interpolate_frames(pre, post)
+        self.aligned[-INTERP_LEN:] = interpolate_frames(pre, post)
         for i in range(OVERLAP, INFER_LEN):
-            d = depth_list[fid + i] * scale + shift
+            d = win[i] * scale + shift
             d[d < 0] = 0
-            aligned.append(d)
-        ref_align = ref_align[:1]
+            self.aligned.append(d)
+        self.ref_align = self.ref_align[:1]
         for kf in kf_align[1:]:
-            d = depth_list[fid + kf] * scale + shift
+            d = win[kf] * scale + shift
             d[d < 0] = 0
-            ref_align.append(d)
-    return np.stack(aligned[:n_frames], axis=0)
+            self.ref_align.append(d)
+        self._flush(INTERP_LEN)
+
+    def result(self) -> np.ndarray:
+        self._flush(0)
+        return self.out[:self.done]
+
+
+def stitch(depth_list: List[np.ndarray], n_frames: int) -> np.ndarray:
+    """depth_list: per-window depth frames concatenated (32 per window) -> [n_frames, h, w]."""
+    st = Stitcher(n_frames)
+    for fid in range(0, len(depth_list), INFER_LEN):
+        st.add(depth_list[fid:fid + INFER_LEN])
+    return st.result()
 
 
 # ---- driver ---------------------------------------------------------------------------------
 class _HostSink:
     """Moves each window's resized depth [32, h, w] off the device as soon as it exists (as the
-    reference does, video_depth.py:372-373), so device memory stays flat in the video length.  On a
-    GPU the copies go through a ring of two pinned staging buffers with non-blocking D2H copies, so
-    the next window's forward is enqueued while the previous window drains."""
+    reference does, video_depth.py:372-373), so device memory stays flat in the video length, and
+    stitches the windows in order as they land.  On a GPU the copies go through a ring of two
+    pinned staging buffers with non-blocking D2H copies: window k is copied out and stitched on the
+    host while the device runs window k + 1's forward."""
 
-    def __init__(self, device: torch.device):
+    def __init__(self, device: torch.device, n_frames: int):
         self.gpu = device.type == "cuda"
         self.ring: list = []
         self.pending: list = []  # (window id, staging slot, event)
-        self.out = {}
+        self.ready = {}          # landed windows not yet stitched (multi-rank rounds arrive out of order)
+        self.next = 0
+        self.stitcher = Stitcher(n_frames)
+
+    def _land(self, k: int, a: np.ndarray):
+        self.ready[k] = a
+        while self.next in self.ready:
+            self.stitcher.add(list(self.ready.pop(self.next)))
+            self.next += 1
 
     def _drain(self, keep: int):
         while len(self.pending) > keep:
             k, slot, ev = self.pending.pop(0)
             ev.synchronize()
-            self.out[k] = slot.numpy().copy()
+            self._land(k, slot.numpy().copy())
 
     def put(self, k: int, d: torch.Tensor):
         if not self.gpu:
-            self.out[k] = d.detach().to("cpu", torch.float32).numpy().copy()
+            self._land(k, d.detach().to("cpu", torch.float32).numpy().copy())
             return
         self._drain(1)  # slot (len(pending) % 2) is free after this
         busy = {id(s) for _, s, _ in self.pending}
@@ -193,9 +232,44 @@ class _HostSink:
         ev.record()
         self.pending.append((k, slot, ev))
 
-    def result(self):
+    def result(self) -> np.ndarray:
         self._drain(0)
-        return self.out
+        if self.ready:
+            raise RuntimeError(f"windows {sorted(self.ready)} never became stitchable (missing {self.next})")
+        return self.stitcher.result()
+
+
+class _HostSource:
+    """Uploads a window batch's frames: gathered on the host into one of two pinned staging
+    buffers, then copied with a non-blocking H2D (a pageable copy would hold the host until the
+    device had drained the previous window, leaving the GPU idle while the next forward is
+    launched).  A slot is reused only after its previous copy has completed."""
+
+    def __init__(self, frames: torch.Tensor, device: torch.device):
+        self.frames, self.dev = frames, device
+        self.gpu = device.type == "cuda"
+        self.slots: list = []  # [pinned tensor, event or None]
+
+    def get(self, idx: List[int]) -> torch.Tensor:
+        ix = torch.as_tensor(idx, dtype=torch.long)
+        if not self.gpu:
+            return self.frames[ix].to(self.dev)
+        shape = (len(idx),) + tuple(self.frames.shape[1:])
+        slot = next((s for s in self.slots if tuple(s[0].shape) == shape and (s[1] is None or s[1].query())), None)
+        if slot is None:
+            if len(self.slots) >= 2:
+                slot = self.slots.pop(0)
+                slot[1].synchronize()
+                if tuple(slot[0].shape) != shape:
+                    slot[0] = torch.empty(shape, dtype=self.frames.dtype, pin_memory=True)
+            else:
+                slot = [torch.empty(shape, dtype=self.frames.dtype, pin_memory=True), None]
+            self.slots.append(slot)
+        torch.index_select(self.frames, 0, ix, out=slot[0])
+        x = slot[0].to(self.dev, non_blocking=True)
+        slot[1] = torch.cuda.Event()
+        slot[1].record()
+        return x
 
 
 def _gather_round(buf: torch.Tensor, rank: int, world: int, group):
@@ -211,7 +285,7 @@ def _gather_round(buf: torch.Tensor, rank: int, world: int, group):
 
 def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, target_fps, input_size: int = 518,
                       device="cuda", windows_per_batch: int = 1, rank: int = 0, world: int = 1, group=None,
-                      io=DeviceIO):
+                      io=DeviceIO, streams: int = 2):
     """Depth for every frame of ``frames`` (uint8 [N, h, w, 3] numpy or tensor).
 
     ``forward(x[B, 32, 3, H, W]) -> depth[B, 32, H, W]`` is the clip forward (the model, or any
@@ -220,6 +294,11 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
     rounds') depth maps are gathered to rank 0 as soon as they exist, so no rank ever holds more than
     one batch of windows on the device.  Rank 0 keeps the windows in host memory and stitches;
     rank 0 returns (depth, fps), others (None, fps).
+
+    ``streams`` > 1 (one GPU, world == 1): consecutive window batches go round-robin onto that many
+    HIP streams, so one window's forward can start while the previous one's tail kernels run (two
+    streams: the 176-frame ViT-L job in 414-420 ms against 442 ms on one stream and 413 ms for its
+    8 forwards back to back; ``tools/video_probe.py``).
     """
     if not isinstance(frames, torch.Tensor):
         frames = torch.from_numpy(np.ascontiguousarray(frames))
@@ -229,27 +308,34 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
     nwin = len(window_starts(n))
     rounds = (nwin + world - 1) // world
     dev = torch.device(device)
-    sink = _HostSink(dev) if rank == 0 else None
+    sink = _HostSink(dev, n) if rank == 0 else None
+    source = _HostSource(frames, dev)
     wpb = max(1, int(windows_per_batch))
-    for r0 in range(0, rounds, wpb):
+    strs = []
+    if dev.type == "cuda" and world == 1 and int(streams) > 1:
+        strs = [torch.cuda.Stream(device=dev) for _ in range(int(streams))]
+        for st in strs:
+            st.wait_stream(torch.cuda.current_stream(dev))
+    for bi, r0 in enumerate(range(0, rounds, wpb)):
         rr = list(range(r0, min(rounds, r0 + wpb)))
         ks = [r * world + rank for r in rr if r * world + rank < nwin]
         d = None
-        if ks:
-            idx = [window_frame_indices(k, n) for k in ks]
-            uniq = sorted(set(i for row in idx for i in row))
-            pre = io.preprocess(frames[uniq].to(dev), size)
-            pos = {f: j for j, f in enumerate(uniq)}
-            x = torch.stack([pre[[pos[i] for i in row]] for row in idx], 0)
-            del pre
-            with torch.no_grad():
-                d = forward(x).float()  # [B, 32, H, W]
-            del x
-            d = io.resize_depth(d.flatten(0, 1), (h, w)).view(len(ks), INFER_LEN, h, w)
-        if world == 1:
-            for j, k in enumerate(ks):
-                sink.put(k, d[j])
-            continue
+        with (torch.cuda.stream(strs[bi % len(strs)]) if strs else contextlib.nullcontext()):
+            if ks:
+                idx = [window_frame_indices(k, n) for k in ks]
+                uniq = sorted(set(i for row in idx for i in row))
+                pre = io.preprocess(source.get(uniq), size)
+                pos = {f: j for j, f in enumerate(uniq)}
+                x = torch.stack([pre[[pos[i] for i in row]] for row in idx], 0)
+                del pre
+                with torch.no_grad():
+                    d = forward(x).float()  # [B, 32, H, W]
+                del x
+                d = io.resize_depth(d.flatten(0, 1), (h, w)).view(len(ks), INFER_LEN, h, w)
+            if world == 1:
+                for j, k in enumerate(ks):
+                    sink.put(k, d[j])
+                continue
         # every rank takes part in every round's gather (a rank without a window sends zeros)
         buf = torch.zeros(len(rr), INFER_LEN, h, w, dtype=torch.float32, device=dev)
         if d is not None:
@@ -263,8 +349,4 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
                         sink.put(k, bufs[src][j])
     if rank != 0:
         return None, target_fps
-    out = sink.result()
-    depth_list = []
-    for k in range(nwin):
-        depth_list += list(out[k])
-    return stitch(depth_list, n), target_fps
+    return sink.result(), target_fps
