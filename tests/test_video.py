@@ -187,3 +187,34 @@ def test_video_device_memory_flat_in_video_length():
         assert d.shape == (n, 48, 64)
         peaks.append(torch.cuda.max_memory_allocated() - base)
     assert peaks[1] <= peaks[0] * 1.1 + (1 << 20), peaks
+
+
+def test_host_sink_stitches_out_of_order_windows():
+    """Multi-rank rounds land windows out of order (windows_per_batch > 1): the incremental stitcher
+    must buffer them and produce exactly the one-shot stitch of the ordered list."""
+    g = np.random.default_rng(5)
+    nwin, n = 5, 100
+    wins = [g.random((V.INFER_LEN, 6, 7), dtype=np.float32) * 10 + 1 for _ in range(nwin)]
+    ref = V.stitch([f for w in wins for f in w], n)
+    sink = V._HostSink(torch.device("cpu"), n)
+    for k in (2, 0, 4, 1, 3):
+        sink.put(k, torch.from_numpy(wins[k]))
+    out = sink.result()
+    assert out.shape == ref.shape == (n, 6, 7)
+    assert np.array_equal(out, ref)
+    # a window that never arrives is an error, not a silently short video
+    sink = V._HostSink(torch.device("cpu"), n)
+    sink.put(1, torch.from_numpy(wins[1]))
+    with pytest.raises(RuntimeError):
+        sink.result()
+
+
+@pytest.mark.gpu
+def test_video_two_streams_identical_to_one():
+    """infer_video_depth(streams=2) runs consecutive windows on two HIP streams: same bytes as one stream."""
+    import vda_amd
+    frames, _, meta = load_video_golden()
+    m = vda_amd.build_model("vits", recipe_state_dict("vits"), device="cuda")
+    d1, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=1)
+    d2, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=2)
+    assert np.array_equal(d1, d2)
