@@ -50,8 +50,8 @@ PROFILE_ROUND = "r02"      # profiles/<round>_pmc_*.json carry the PMC figures q
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--encoder", default="vitl")
     ap.add_argument("--frames", type=int, default=32)
     ap.add_argument("--size", type=int, nargs=2, default=[518, 518], metavar=("H", "W"))
