@@ -689,13 +689,14 @@ class _StreamEngine:
 
 
 def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", fp32=False, skip_tmp_block=False,
-                       windows_per_batch=1, rank=0, world=1, group=None):
+                       windows_per_batch=1, rank=0, world=1, group=None, streams=2):
     """video_depth.py:329-417 on the MI355X forward (see vda_amd.video); ``fp32=True`` runs the
-    fp32 kernels (the reference's autocast-off path), the default fp16 compute."""
+    fp32 kernels (the reference's autocast-off path), the default fp16 compute; ``streams``: window
+    batches in flight on one GPU (world == 1)."""
     from .video import infer_video_depth
     return infer_video_depth(lambda x: self.forward(x, skip_tmp_block, fp32=fp32), frames, target_fps, input_size=input_size,
                              device=device, windows_per_batch=windows_per_batch, rank=rank, world=world,
-                             group=group)
+                             group=group, streams=streams)
 
 
 VideoDepthAnything.infer_video_depth = _infer_video_depth
