@@ -218,3 +218,14 @@ def test_video_two_streams_identical_to_one():
     d1, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=1)
     d2, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=2)
     assert np.array_equal(d1, d2)
+
+
+@pytest.mark.gpu
+def test_video_frames_already_on_device():
+    """frames may be handed over as a device tensor (no host staging then): same result as numpy."""
+    def fwd(x):
+        return x[:, :, 0].contiguous()
+    frames = np.random.default_rng(3).integers(0, 256, (40, 48, 64, 3), dtype=np.uint8)
+    d_host, _ = V.infer_video_depth(fwd, frames, 24, input_size=56, device="cuda")
+    d_dev, _ = V.infer_video_depth(fwd, torch.from_numpy(frames).cuda(), 24, input_size=56, device="cuda")
+    assert np.array_equal(d_host, d_dev)

@@ -252,8 +252,8 @@ class _HostSource:
 
     def get(self, idx: List[int]) -> torch.Tensor:
         ix = torch.as_tensor(idx, dtype=torch.long)
-        if not self.gpu:
-            return self.frames[ix].to(self.dev)
+        if not self.gpu or self.frames.device.type != "cpu":  # CPU run, or frames already on a device
+            return self.frames[ix.to(self.frames.device)].to(self.dev)
         shape = (len(idx),) + tuple(self.frames.shape[1:])
         slot = next((s for s in self.slots if tuple(s[0].shape) == shape and (s[1] is None or s[1].query())), None)
         if slot is None:
