@@ -224,10 +224,24 @@ def main():
         for _ in range(2):
             model(x)
         torch.cuda.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            out_static = model(x)
-        fn = lambda i: (graph.replay(), out_static)[1]  # noqa: E731
+        # one captured forward per clip-in-flight stream (each graph owns its memory pool), replayed
+        # on that stream
+        graphs, outs = [], []
+        for st in (strs or [None]):
+            g_ = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_, stream=st):
+                outs.append(model(x))
+            graphs.append(g_)
+        torch.cuda.synchronize()
+
+        def fn(i):
+            j = i % len(graphs)
+            if strs:
+                with torch.cuda.stream(strs[j]):
+                    graphs[j].replay()
+            else:
+                graphs[j].replay()
+            return outs[j]
 
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     for i in range(args.warmup):
