@@ -1373,7 +1373,15 @@ int launch_act(const GemmParams& p, hipStream_t st) {  // returns the tile confi
     else if (p.N == 128 && p.M >= 8192 && a16 && dense_ok && e.store == VDA_STORE_ROWS && !e.ln_stats) cfg = 5;
     else if (p.N >= 256 && p.M >= 4096) cfg = 3;
     else if (p.N >= 128 && p.M >= 4096) cfg = 1;
-    else cfg = 0;
+    else if (CONV) cfg = 0;
+    else {
+      // small M (the streaming mode's one-frame encoder, M = 1,370): the largest tile that still
+      // gives >= 2 tiles per CU, else 64x64 (tools/bench_gemm_small.py: ViT-L fc2 72.8 -> 43.5 us,
+      // proj 24.0 -> 14.0, qkv 29.5 -> 25.0, fc1 34.2 -> 30.3)
+      const long ncu2 = 2L * cu_count();
+      auto ntiles = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
+      cfg = ntiles(128, 128) >= ncu2 ? 0 : ntiles(128, 64) >= ncu2 ? 2 : 6;
+    }
   }
   switch (cfg) {
     case 1: launch_tile<256, 128, 4, 2, 32, 4, CONV, ACT>(p, st); break;
@@ -1381,6 +1389,8 @@ int launch_act(const GemmParams& p, hipStream_t st) {  // returns the tile confi
     case 3: launch_tile<256, 256, 2, 4, 32, 4, CONV, ACT>(p, st); break;
     case 4: launch_phased<2, 2, CONV, ACT>(p, st); break;
     case 5: launch_phased<4, 1, CONV, ACT>(p, st); break;
+    case 6: launch_tile<64, 64, 2, 2, 32, 4, CONV, ACT>(p, st); break;
+    case 7: launch_tile<64, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
     default: launch_tile<128, 128, 2, 2, 32, 4, CONV, ACT>(p, st); break;
   }
   return cfg;
