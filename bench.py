@@ -12,6 +12,9 @@ collective stream, overlapped with the next step's forward).  The timed region i
 barrier + synchronize; the MAX over ranks is taken; value = all ranks' frames / that time
 ("scaling": "weak").  ``--gpus N`` without torchrun's WORLD_SIZE re-launches this script under
 ``torch.distributed.run`` with N ranks (as a child process, before anything touches the GPU).
+``--streams S`` (default 2): S clips in flight per GPU — step i runs on HIP stream i % S, so one
+clip's low-occupancy kernels and partial last rounds share the CUs with the other clip's; every
+step is still one whole forward, all inside the timed region.
 
 ``--video`` (BASELINE configs[3] as a video job): a synthetic 176-frame 518x518 uint8 video through
 ``infer_video_depth`` (GPU preprocessing, 8 overlapping 32-frame windows sharded round-robin over the
@@ -20,7 +23,8 @@ timed region.  value = video frames / s ("scaling": "strong": the video is fixed
 
 Extra fields:
   roofline      dominant kernel = encoder MLP fc1 GEMM + GELU, timed per launch with HIP events on its
-                launch stream inside the timed region; achieved = algorithmic FLOPs per launch / mean
+                launch stream (inside the timed region with one clip in flight; with several, over
+                single-stream forwards right after it, see roofline.probe); achieved = algorithmic FLOPs per launch / mean
                 launch time vs 2.5 PFLOP/s dense fp16; traffic from profiles/<round>_pmc_fc1.json
                 (rocprofv3 PMC, gfx950-corrected), mfma_busy_pmc from profiles/<round>_pmc_mfma.json
   cpu_baseline  the oracle's fp32 PyTorch-CPU forward (oracle/vda_oracle.py) of one full clip of the
