@@ -268,7 +268,9 @@ int vda_debug_force_tile(int32_t cfg);
 /*
  * Tuning hook for the phased 256-row GEMM: persist_blocks > 0 launches that many persistent blocks
  * (0 = one block per tile, -1 = automatic: one per CU); stagger_ticks >= 0 forces the start delay
- * (100 MHz ticks) of the delayed half of the blocks (-1 = automatic).  Process-global; for tuning.
+ * (100 MHz ticks) of the delayed half of the blocks, -1 = automatic (none: the drivers run two clips
+ * in flight), -2 = half a tile when the last round is short (the one-clip optimum).  Process-global;
+ * for tuning.
  */
 int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
 /* Tuning experiment: with groups > 1 every phased-GEMM block starts ((block / 8) % groups) / groups of

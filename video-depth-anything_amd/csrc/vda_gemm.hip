@@ -1312,11 +1312,16 @@ void phased_sched(int ntiles, int nk, bool conv, int& grid, int& ticks) {
   // measured in situ: persistent pays for the dense GEMMs, one block per tile for the convs
   const int persist = conv ? 0 : (g_persist >= 0 ? g_persist : cus);
   grid = persist == 0 ? ntiles : std::min(ntiles, persist);
+  // The start stagger for a short last round (half the blocks with one tile fewer start half a
+  // tile late, ~1.45 us per 64-deep K step + ~6 us prologue/epilogue) is off by default: it is worth
+  // +0.4 % with one clip in flight but -0.6 % with the two clips in flight the drivers run (the
+  // sleeping blocks hold CUs the other clip's kernels would use).  vda_debug_gemm_sched(-1, -2)
+  // restores it, a value >= 0 forces that many 100-MHz ticks.
   ticks = 0;
+  (void)nk;
   if (g_stagger >= 0) {
     ticks = g_stagger;
-  } else if (ntiles > grid && ntiles % grid <= grid / 2) {
-    // half a tile: ~1.45 us per 64-deep K step + ~6 us prologue/epilogue at the clock MFMA runs
+  } else if (g_stagger == -2 && ntiles > grid && ntiles % grid <= grid / 2) {
     ticks = (int)((nk * 1.45f + 6.f) * 0.5f * 100.f);
   }
 }
