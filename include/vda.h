@@ -64,20 +64,23 @@ typedef struct vda_epilogue {
    * row stream x, W holds gamma (.) W_ln, bias holds W_ln beta + b, ln_colsum[n] = sum_k W[n, k] (of the
    * fp16 W actually used), and ln_stats[m] = (mean, rstd) of row m from vda_row_stats.  Then
    * rstd (x W^T - mean colsum) + bias = LN(x) W_ln^T + b exactly in real arithmetic.  ln_stats holds
-   * an even number of rows (M rounded up to 2).  Row store only, no gamma, activation none/gelu/relu. */
+   * an even number of rows (M rounded up to 2).  Row store only, no gamma / rowbias, activation
+   * none / gelu. */
   const float* ln_stats;  /* [round_up(M, 2), 2] or NULL                              */
   const float* ln_colsum; /* [N]                                                     */
   /* ln_parts > 0: ln_stats instead holds [M, ln_parts, 2] partial (sum, sum of squares) of row m
    * over ln_parts column blocks (as written through stats_out by the GEMM that produced X); the
    * epilogue forms mean = sum / K, var = max(sumsq / K - mean^2, 0), rstd = 1 / sqrt(var + ln_eps).
-   * ln_parts <= 4. */
+   * ln_parts <= 4.  The partials are staged in 16-byte pieces: the buffer must extend to a multiple
+   * of 4 floats (one spare row when M * ln_parts is odd). */
   int32_t ln_parts;
   float ln_eps;
   /* Producer side: write [M, ceil(N / 256), 2] per-row partial (sum, sum of squares) of the fp16
    * OUTPUT values (after the residual adds) over 256-column blocks, for a following LN-folded GEMM
    * (ln_parts = ceil(N / 256)): the statistics pass over the row stream is never a separate read.
-   * Row store, no pixel shuffle; computed by a separate partial-sum kernel when the GEMM shape does
-   * not take the phased 256x256 kernel. */
+   * Row store, no pixel shuffle, no GEGLU; computed by a separate partial-sum kernel when the GEMM
+   * shape does not take the phased 256x256 kernel (then N % 8 == 0, ldy % 8 == 0, y 16-byte aligned).
+   * Not available in the fp32 entry points. */
   float* stats_out;
 } vda_epilogue;
 
@@ -273,6 +276,10 @@ int vda_debug_force_tile(int32_t cfg);
  * for tuning.
  */
 int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
+/* Tuning hook for the two-blocks-per-CU encoder GEMM (gemm2_kernel): mode -1 = automatic, 0 = never,
+ * 1 = every shape it serves; start_ticks = start offset (100 MHz ticks) of the second half of its
+ * blocks.  Process-global; for tests and A/B runs. */
+int vda_debug_gemm2(int32_t mode, int32_t start_ticks);
 /* Tuning experiment: with groups > 1 every phased-GEMM block starts ((block / 8) % groups) / groups of
  * the stagger ticks late (desynchronises the CUs' epilogue store bursts).  0 = off. */
 int vda_debug_gemm_desync(int32_t groups);

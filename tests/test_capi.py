@@ -35,6 +35,21 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_integration_doc_binding_matches_library():
+    """INTEGRATION.md's ctypes stub is what a maintainer copies: its Epilogue mirror must have the
+    library's sizeof(vda_epilogue) and the field order of _lib.Epilogue (a short struct makes
+    vda_gemm read past it)."""
+    doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    m = re.search(r"class Epilogue\(ctypes\.Structure\):.*?_fields_ = (\[.*?\])\n", doc, re.S)
+    assert m, "INTEGRATION.md has no Epilogue mirror"
+    fields = eval(m.group(1), {"ctypes": ctypes})  # the doc's own literal, ctypes types only
+    Doc = type("DocEpilogue", (ctypes.Structure,), {"_fields_": fields})
+    assert [f[0] for f in fields] == [f[0] for f in _lib.Epilogue._fields_]
+    assert [f[1] for f in fields] == [f[1] for f in _lib.Epilogue._fields_]
+    assert ctypes.sizeof(Doc) == _lib.lib().vda_epilogue_size()
+    assert "vda_epilogue_size()" in doc  # the stub checks its mirror against the library
+
+
 def test_version_and_error_plumbing():
     lib = _lib.lib()
     assert b"gfx950" in lib.vda_version()
@@ -56,6 +71,23 @@ def test_gemm_argument_validation(args, msg):
     rc = lib.vda_gemm(fake, ldx, fake, fake, ldy, M, N, K, _lib.Epilogue(), None)
     assert rc == -22
     assert msg in lib.vda_last_error()
+
+
+def test_epilogue_combinations_rejected():
+    """Epilogue options no kernel route implements are rejected up front: the LN fold
+    with ReLU or a row bias, row statistics with GEGLU (its output is N/2 wide) or in fp32 mode."""
+    lib = _lib.lib()
+    fake = ctypes.c_void_p(0x1000)
+    e = _lib.Epilogue(rdiv=1, rmod=1, ln_stats=0x2000, ln_colsum=0x3000, act=_lib.ACT_RELU)
+    assert lib.vda_gemm(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
+    assert b"ln_stats" in lib.vda_last_error()
+    e = _lib.Epilogue(rdiv=1, rmod=1, ln_stats=0x2000, ln_colsum=0x3000, rowbias=0x4000)
+    assert lib.vda_gemm(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
+    e = _lib.Epilogue(rdiv=1, rmod=1, stats_out=0x2000, act=_lib.ACT_GEGLU)
+    assert lib.vda_gemm(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
+    assert b"stats_out" in lib.vda_last_error()
+    e = _lib.Epilogue(rdiv=1, rmod=1, stats_out=0x2000)
+    assert lib.vda_gemm_f32(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
 
 
 def test_conv_and_attention_validation():

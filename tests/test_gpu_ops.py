@@ -613,7 +613,7 @@ def test_gemm_epilogue_row_stats(M, N, K):
     r = (torch.randn(M, N, generator=g) * 2 + torch.randn(M, 1, generator=g)).half()
     P = (N + 255) // 256
     tok = r.to(DEV).contiguous()
-    st = torch.full((M, P, 2), float("nan"), device=DEV)
+    st = torch.full((M + 1, P, 2), float("nan"), device=DEV)  # spare row: 16-byte staging (vda.h ln_parts)
     ops.gemm(h(x), h(w), bias=f32(b), res=tok, out=tok, stats_out=st)
     y = tok.float().cpu()
     pad = torch.zeros(M, P * 256)

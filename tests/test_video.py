@@ -79,16 +79,22 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, q):
+def _rank_main(rank, world, port, q, wpb=1, single=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.set_num_threads(2)
     frames, _, meta = load_video_golden()
     sd = recipe_state_dict("vits")
     depth, _ = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
-                                   device="cpu", rank=rank, world=world, io=vda_oracle.TorchIO)
+                                   device="cpu", rank=rank, world=world, io=vda_oracle.TorchIO, streams=2,
+                                   windows_per_batch=wpb)
     if rank == 0:
-        q.put(depth)
+        if single:  # the same job in one process, same threads: the sharded result must be these bytes
+            d1, _ = V.infer_video_depth(_oracle_forward(sd), frames, meta["fps"], input_size=meta["input_size"],
+                                        device="cpu", io=vda_oracle.TorchIO, streams=2)
+            q.put((depth, d1))
+        else:
+            q.put(depth)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -107,6 +113,24 @@ def test_clip_parallel_gloo_world2_matches_single_process():
         assert p.exitcode == 0
     err = float(np.abs(depth - depth_ref).sum() / np.abs(depth_ref).sum())
     assert err <= 1e-5, err
+
+
+def test_clip_parallel_gloo_world2_async_gather_byte_identical():
+    """World 2 with streams=2: each round's gather is asynchronous and rank 0 stitches a round only
+    after the next round's forward and gather are enqueued; the result is byte for byte the
+    single-process job's (video_depth.py:358-413; one window per forward on both sides, so every
+    window's clip forward is the same computation)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q, 1, True)) for r in range(2)]
+    for p in procs:
+        p.start()
+    depth, d1 = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert depth.shape == d1.shape and np.array_equal(depth, d1)
 
 
 @pytest.mark.gpu
@@ -218,6 +242,22 @@ def test_video_two_streams_identical_to_one():
     d1, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=1)
     d2, _ = V.infer_video_depth(m, frames, meta["fps"], input_size=meta["input_size"], device="cuda", streams=2)
     assert np.array_equal(d1, d2)
+
+
+@pytest.mark.gpu
+def test_video_two_streams_fresh_model():
+    """streams=2 as the FIRST call on a freshly built model: the packed weights and the
+    resolution's token bias are built on the current stream before the side streams start, so the
+    result equals a fresh model's one-stream run."""
+    import vda_amd
+    frames, _, meta = load_video_golden()
+    d = []
+    for streams in (2, 1):
+        m = vda_amd.build_model("vits", recipe_state_dict("vits"), device="cuda")
+        d.append(m.infer_video_depth(frames, meta["fps"], input_size=meta["input_size"], device="cuda",
+                                     streams=streams)[0])
+        del m
+    assert np.array_equal(d[0], d[1])
 
 
 @pytest.mark.gpu

@@ -522,6 +522,7 @@ extern "C" int vda_gemm_f32(const float* x, int64_t ldx, const float* w, float* 
                 "bad pixel-shuffle geometry");
   VDA_CHECK_ARG(!epi->rowbias || (epi->rdiv > 0 && epi->rmod > 0), "rowbias needs rdiv, rmod > 0");
   VDA_CHECK_ARG(!epi->ln_stats, "fp32 GEMM: no LayerNorm fold (the fp32 mode runs vda_layernorm_f32)");
+  VDA_CHECK_ARG(!epi->stats_out, "fp32 GEMM: no row statistics output");
   F32Params p{};
   p.x = x; p.ldx = ldx; p.w = w; p.y = y; p.ldy = ldy; p.M = M; p.N = N; p.K = K; p.epi = *epi;
   return launch_f32<false>(p, (hipStream_t)stream);

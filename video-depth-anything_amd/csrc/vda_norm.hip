@@ -341,6 +341,9 @@ extern "C" int vda_row_stats(const void* x, int64_t ldx, float* stats, int32_t r
 }
 
 int vda_row_partials_launch(const void* y, int64_t ldy, float* out, int32_t rows, int32_t N, hipStream_t stream) {
+  // the kernel reads whole 16-byte pieces of y
+  VDA_CHECK_ARG(N % 8 == 0 && ldy % 8 == 0 && (uintptr_t)y % 16 == 0,
+                "stats_out: the output needs N % 8 == 0, ldy % 8 == 0 and 16-byte alignment");
   const int P = (N + 255) / 256;
   const long items = (long)rows * P;
   hipLaunchKernelGGL(row_partials_kernel, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, stream,

@@ -434,6 +434,15 @@ class VideoDepthAnything(nn.Module):
         self._pos_cache[key] = tb
         return tb
 
+    @torch.no_grad()
+    def prepare(self, device, size, fp32: bool = False) -> None:
+        """Build, on the current stream, the state a forward at net input ``size`` = (H, W) would
+        create lazily: the packed weights and the token bias of that resolution.  The video driver
+        calls it before it spreads windows over several streams (a side stream must not read them
+        while the first forward is still writing them)."""
+        P = self._pack(torch.device(device), fp32)
+        self._token_bias(P, int(size[0]), int(size[1]), torch.device(device))
+
     # -- forward ---------------------------------------------------------------------------
     def _temporal(self, q: _Packed, x: torch.Tensor, B: int, T: int, S: int) -> torch.Tensor:
         """TemporalModule on token-major frames x [B*T*S, C] (motion_module.py:64-133)."""
@@ -499,7 +508,8 @@ class VideoDepthAnything(nn.Module):
         nparts = (C + 255) // 256
         epistats = P.lnfold and nparts <= 4 and os.environ.get("VDA_NO_EPISTATS", "0") != "1"
         if epistats:
-            st_a = torch.empty(tok.shape[0], nparts, 2, device=tok.device, dtype=torch.float32)
+            # one spare row: the LN-folded GEMMs stage the partials in 16-byte pieces (vda.h ln_parts)
+            st_a = torch.empty(tok.shape[0] + 1, nparts, 2, device=tok.device, dtype=torch.float32)
             st_b = torch.empty_like(st_a)
         stats, parts = None, 0
         for i, q in enumerate(P.blocks):
@@ -696,7 +706,7 @@ def _infer_video_depth(self, frames, target_fps, input_size=518, device="cuda", 
     from .video import infer_video_depth
     return infer_video_depth(lambda x: self.forward(x, skip_tmp_block, fp32=fp32), frames, target_fps, input_size=input_size,
                              device=device, windows_per_batch=windows_per_batch, rank=rank, world=world,
-                             group=group, streams=streams)
+                             group=group, streams=streams, prepare=lambda hw: self.prepare(device, hw, fp32))
 
 
 VideoDepthAnything.infer_video_depth = _infer_video_depth

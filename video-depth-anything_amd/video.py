@@ -273,32 +273,36 @@ class _HostSource:
 
 
 def _gather_round(buf: torch.Tensor, rank: int, world: int, group):
-    """Gather one round's per-rank window buffers [n, 32, h, w] to rank 0 (RCCL on GPU tensors; gloo
-    takes host copies).  Returns the list of world buffers on rank 0, None elsewhere."""
+    """Start gathering one round's per-rank window buffers [n, 32, h, w] to rank 0 (RCCL on GPU
+    tensors, issued on the current stream; gloo takes host copies).  Returns (the list of world
+    receive buffers on rank 0 or None, the async work, the send buffer to keep alive)."""
     import torch.distributed as dist
     cpu = dist.get_backend(group) == "gloo"
     src = buf.cpu() if cpu else buf
     bufs = [torch.empty_like(src) for _ in range(world)] if rank == 0 else None
-    dist.gather(src, bufs, dst=0, group=group)
-    return bufs
+    work = dist.gather(src, bufs, dst=0, group=group, async_op=True)
+    return bufs, work, src
 
 
 def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, target_fps, input_size: int = 518,
                       device="cuda", windows_per_batch: int = 1, rank: int = 0, world: int = 1, group=None,
-                      io=DeviceIO, streams: int = 2):
+                      io=DeviceIO, streams: int = 2, prepare: Optional[Callable[[tuple], None]] = None):
     """Depth for every frame of ``frames`` (uint8 [N, h, w, 3] numpy or tensor).
 
     ``forward(x[B, 32, 3, H, W]) -> depth[B, 32, H, W]`` is the clip forward (the model, or any
-    callable).  With world > 1, window k runs on rank k % world: round r is windows
+    callable); ``prepare((H, W))``, when given, builds whatever state the forward creates lazily
+    (packed weights, the resolution's token bias) on the current stream before any side stream runs
+    a forward.  With world > 1, window k runs on rank k % world: round r is windows
     r*world .. r*world + world - 1, one per rank, and each round's (or each ``windows_per_batch``
-    rounds') depth maps are gathered to rank 0 as soon as they exist, so no rank ever holds more than
-    one batch of windows on the device.  Rank 0 keeps the windows in host memory and stitches;
-    rank 0 returns (depth, fps), others (None, fps).
+    rounds') depth maps are gathered to rank 0 by an asynchronous collective, so no rank ever holds
+    more than two batches of windows on the device.  Rank 0 hands round r's windows to the host
+    stitcher only after round r + 1's forward and gather are enqueued, so the host work never sits
+    between two collectives; rank 0 returns (depth, fps), others (None, fps).
 
-    ``streams`` > 1 (one GPU, world == 1): consecutive window batches go round-robin onto that many
-    HIP streams, so one window's forward can start while the previous one's tail kernels run (two
-    streams: the 176-frame ViT-L job in 414-420 ms against 442 ms on one stream and 413 ms for its
-    8 forwards back to back; ``tools/video_probe.py``).
+    ``streams`` > 1 (GPU): consecutive window batches go round-robin onto that many HIP streams, so
+    one window's forward can start while the previous one's tail kernels run (one GPU, two streams:
+    the 176-frame ViT-L job in 414-420 ms against 442 ms on one stream and 413 ms for its 8 forwards
+    back to back; ``tools/video_probe.py``).  Each rank of a multi-GPU job does the same.
     """
     if not isinstance(frames, torch.Tensor):
         frames = torch.from_numpy(np.ascontiguousarray(frames))
@@ -311,11 +315,27 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
     sink = _HostSink(dev, n) if rank == 0 else None
     source = _HostSource(frames, dev)
     wpb = max(1, int(windows_per_batch))
+    if prepare is None and callable(getattr(forward, "prepare", None)):  # the model itself as the forward
+        prepare = lambda hw: forward.prepare(dev, hw)  # noqa: E731
+    if prepare is not None:
+        prepare(size)
     strs = []
-    if dev.type == "cuda" and world == 1 and int(streams) > 1:
+    if dev.type == "cuda" and int(streams) > 1:
         strs = [torch.cuda.Stream(device=dev) for _ in range(int(streams))]
-        for st in strs:
+        for st in strs:  # after prepare(): the side streams see the packed weights / token bias
             st.wait_stream(torch.cuda.current_stream(dev))
+    pending = None  # previous round's (receive buffers, rounds, work, send buffer)
+
+    def land(pend):
+        bufs, rr_, work, _ = pend
+        work.wait()  # the current stream (or, on gloo, the host) waits for the gather
+        if rank == 0:
+            for src in range(world):
+                for j, r in enumerate(rr_):
+                    k = r * world + src
+                    if k < nwin:
+                        sink.put(k, bufs[src][j])
+
     for bi, r0 in enumerate(range(0, rounds, wpb)):
         rr = list(range(r0, min(rounds, r0 + wpb)))
         ks = [r * world + rank for r in rr if r * world + rank < nwin]
@@ -336,17 +356,17 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
                 for j, k in enumerate(ks):
                     sink.put(k, d[j])
                 continue
-        # every rank takes part in every round's gather (a rank without a window sends zeros)
-        buf = torch.zeros(len(rr), INFER_LEN, h, w, dtype=torch.float32, device=dev)
-        if d is not None:
-            buf[:len(ks)] = d
-        bufs = _gather_round(buf, rank, world, group)
-        if rank == 0:
-            for src in range(world):
-                for j, r in enumerate(rr):
-                    k = r * world + src
-                    if k < nwin:
-                        sink.put(k, bufs[src][j])
+            # every rank takes part in every round's gather (a rank without a window sends zeros),
+            # enqueued behind this round's forward on its stream
+            buf = torch.zeros(len(rr), INFER_LEN, h, w, dtype=torch.float32, device=dev)
+            if d is not None:
+                buf[:len(ks)] = d
+            cur = _gather_round(buf, rank, world, group) + (rr,)
+        if pending is not None:
+            land(pending)
+        pending = (cur[0], cur[3], cur[1], cur[2])
+    if pending is not None:
+        land(pending)
     if rank != 0:
         return None, target_fps
     return sink.result(), target_fps
