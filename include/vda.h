@@ -280,6 +280,9 @@ int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
  * 1 = every shape it serves; start_ticks = start offset (100 MHz ticks) of the second half of its
  * blocks.  Process-global; for tests and A/B runs. */
 int vda_debug_gemm2(int32_t mode, int32_t start_ticks);
+/* Tuning hook for the spatial attention: 0 = the 4-wave kernel (two blocks per CU), 1 = the 8-wave
+ * ping-pong kernel.  Process-global; for tests and A/B runs. */
+int vda_debug_attn(int32_t mode);
 /* Tuning experiment: with groups > 1 every phased-GEMM block starts ((block / 8) % groups) / groups of
  * the stagger ticks late (desynchronises the CUs' epilogue store bursts).  0 = off. */
 int vda_debug_gemm_desync(int32_t groups);

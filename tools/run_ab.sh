@@ -1,7 +1,7 @@
 #!/bin/bash
-# A/B of the encoder GEMMs: in-tree phased vs the 2-blocks-per-CU kernel (2 and 1 block per CU).
+# GEMM register epilogues: op tests, A/B vs round-2 kernel, full-size parity, bench
 set -o pipefail
-python -c "
-import ctypes; l=ctypes.CDLL('build/g2/libvda_c.so'); import torch; torch.zeros(1,device='cuda')
-print('occupancy fc1/fc2 blocks per CU:', l.vda_debug_gemm2(99, 0))"
-timeout -k 10 300 python tools/ab_gemm.py video-depth-anything_amd/libvda.so build/g2/libvda.so@g2=0 build/g2/libvda_b.so@g2m2=0 --rounds 5 --shapes fc2,fc1 > gpurun_out/ab_gemm.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_gemm.log; exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_gpu_ops.py -x -q --timeout 120 --timeout-method thread -k "gemm" > gpurun_out/ab_tests.log 2>&1; rc=$?; tail -2 gpurun_out/ab_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python tools/ab_gemm.py build/base/libvda.so video-depth-anything_amd/libvda.so --rounds 7 > gpurun_out/ab_gemm.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/ab_gemm.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_fullsize.py tests/test_gpu_model.py -x -q -s --timeout 300 --timeout-method thread > gpurun_out/ab_full.log 2>&1; rc=$?; grep -E "rel|passed|failed" gpurun_out/ab_full.log | tail -12; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py > gpurun_out/ab_bench.log 2>&1 && tail -1 gpurun_out/ab_bench.log | cut -c1-250

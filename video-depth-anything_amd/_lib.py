@@ -26,7 +26,7 @@ EXPORTED = (
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
-    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_gemm2", "vda_debug_strip_split",
+    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_gemm2", "vda_debug_attn", "vda_debug_strip_split",
     "vda_debug_hconv", "vda_debug_dconv",
 )
 
@@ -93,6 +93,7 @@ def _declare(lib):
         "vda_debug_gemm_sched": ([I, I], I),
         "vda_debug_gemm_desync": ([I], I),
         "vda_debug_gemm2": ([I, I], I),
+        "vda_debug_attn": ([I], I),
         "vda_debug_strip_split": ([I], I),
         "vda_debug_hconv": ([I], I),
         "vda_debug_dconv": ([I], I),

@@ -1002,6 +1002,196 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   TS(3);
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
+  if constexpr (EK == 1 && XR == 2 && WR == 2) {
+    // Register epilogue (qkv, fc1): no LDS staging.  The LN statistics of the lane's 8 rows come out of
+    // LDS first; then one barrier frees the operand buffers and the next tile's prologue DMA goes out
+    // at once, landing under this tile's activation work and stores.  Pairs of accumulators (channels
+    // 16i.. and 16(i+1)..) are exchanged across 16-lane rows with v_permlane16_swap, after which every
+    // lane holds 8 consecutive channels of its row: one 16-byte store per pair (16 rows x 64 B per wave
+    // instruction; the two pairs of a row fill its 128-B line).
+    const vda_epilogue& e = p.epi;
+    float2 mr[8];
+    if constexpr (LNF) {
+      const float* st = reinterpret_cast<const float*>(lnst_lds);
+      const int P = e.ln_parts;
+      const float invK = 1.f / (float)p.K;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int rl = wm * 128 + j * 16 + mcol;
+        if (P <= 0) {
+          mr[j] = *reinterpret_cast<const float2*>(st + 2 * rl);
+        } else {
+          float sm = 0.f, sq = 0.f;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + (t < P ? t : 0)));
+            sm += t < P ? pq.x : 0.f;
+            sq += t < P ? pq.y : 0.f;
+          }
+          const float mean = sm * invK;
+          mr[j] = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq * invK), 0.f) + e.ln_eps));
+        }
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS read of this tile (operands, statistics) is done
+    __builtin_amdgcn_s_barrier();
+    if constexpr (!CONV) {
+      if (vb_next >= 0) {
+        int tmn, tnn;
+        tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
+        unsigned xn[XR][2], wn2[WR][2];
+        dense_offsets(tmn * BM, tnn * BN, xn, wn2);
+        lnst_dma(tmn * BM);
+        bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
+        if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+      }
+    }
+    static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
+    const int g = lane >> 4;
+    const long mrows = p.M - m0;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(p.y + (long)m0 * p.ldy), (short)0,
+        (int)(mrows * p.ldy * 2 < 0x7fffffffL ? mrows * p.ldy * 2 : 0x7fffffffL), 0x00020000);
+    unsigned cofs[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      const int col = n0 + wn * 64 + 32 * pp + 16 * (g & 1) + 8 * (g >> 1);
+      cofs[pp] = col < p.N ? (unsigned)(col * 2) : 0x80000000u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned rofs = (unsigned)((wm * 128 + j * 16 + mcol) * p.ldy * 2);
+      f4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = acc[i][j];
+        if constexpr (LNF) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[i][r] = fmaf(mr[j].y, fmaf(-mr[j].x, pgv[i][r], v[i][r]), pbv[i][r]);
+        } else {
+          v[i] += pbv[i];
+        }
+        if constexpr (ACT == VDA_ACT_GELU && TAB) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[i][r] = gelu_tab(v[i][r], phib);
+        } else if constexpr (ACT == VDA_ACT_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[i][r] = gelu_erf(v[i][r]);
+        }
+      }
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        float a[4], c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = v[2 * pp][r];
+          c[r] = v[2 * pp + 1][r];
+          perm16_swap(a[r], c[r]);
+        }
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
+        const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
+        const u32x4 o = {__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                         __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+        __builtin_amdgcn_raw_buffer_store_b128(o, ry, rofs + cofs[pp], 0, VDA_EPI_STORE_AUX);
+      }
+    }
+    TS(5);
+    return;
+  }
+  if constexpr (EK == 2 && XR == 2 && WR == 2) {
+    // Register epilogue with one residual and the row statistics (proj, fc2: x += ...): the residual
+    // rows are requested first (in the same 8-consecutive-channel layout the permlane swap produces),
+    // then the operand buffers are handed to the next tile's prologue DMA as above.  Output =
+    // fp16(acc + bias) + residual in packed fp16, as the staged epilogue.  Row statistics: (sum, sumsq)
+    // of the stored fp16 values per lane, over the 4 lanes of a row by permlane swaps, over the 4 waves
+    // of a 256-column block through an 8-KiB LDS table.
+    const vda_epilogue& e = p.epi;
+    const int g = lane >> 4;
+    const long mrows = p.M - m0;
+    auto rsrc_rows = [&](const void* base, long ld) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)((const h16*)base + (long)m0 * ld), (short)0,
+                                               (int)(mrows * ld * 2 < 0x7fffffffL ? mrows * ld * 2 : 0x7fffffffL), 0x00020000);
+    };
+    int ccol[2];
+    bool cok[2];
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      ccol[pp] = n0 + wn * 64 + 32 * pp + 16 * (g & 1) + 8 * (g >> 1);
+      cok[pp] = ccol[pp] < p.N;
+    }
+    const __amdgpu_buffer_rsrc_t rr = rsrc_rows(e.res, e.ldres);
+    h8 rv[8][2];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const unsigned o = cok[pp] ? (unsigned)((((long)(wm * 128 + j * 16 + mcol)) * e.ldres + ccol[pp]) * 2) : 0x80000000u;
+        rv[j][pp] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
+      }
+    __builtin_amdgcn_s_barrier();  // every wave is done reading the operand buffers
+    if constexpr (!CONV) {
+      if (vb_next >= 0) {
+        int tmn, tnn;
+        tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
+        unsigned xn[XR][2], wn2[WR][2];
+        dense_offsets(tmn * BM, tnn * BN, xn, wn2);
+        bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
+        if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+      }
+    }
+    static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
+    const __amdgpu_buffer_rsrc_t ry = rsrc_rows(p.y, p.ldy);
+    float* red = reinterpret_cast<float*>(smem + 2 * BUF);  // [4 wn][256 rows][2]
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int rl = wm * 128 + j * 16 + mcol;
+      float ssum = 0.f, ssq = 0.f;
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        float a[4], c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = acc[2 * pp][j][r] + pbv[2 * pp][r];
+          c[r] = acc[2 * pp + 1][j][r] + pbv[2 * pp + 1][r];
+          perm16_swap(a[r], c[r]);
+        }
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
+        const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
+        const h8 t = __builtin_bit_cast(h8, make_uint4(__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                                                       __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3))) +
+                     rv[j][pp];
+        const unsigned o = cok[pp] ? (unsigned)((((long)rl) * p.ldy + ccol[pp]) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, o, 0, VDA_EPI_STORE_AUX);
+        float s1, q1;
+        stat_acc(cok[pp] ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, s1, q1);
+        ssum += s1;
+        ssq += q1;
+      }
+      // the row's 64 channels of this wave sit in lanes mcol, mcol + 16, + 32, + 48
+      float x0, x1;
+      swap16_pair(ssum, x0, x1); ssum = x0 + x1;
+      swap16_pair(ssq, x0, x1); ssq = x0 + x1;
+      swap32_pair(ssum, x0, x1); ssum = x0 + x1;
+      swap32_pair(ssq, x0, x1); ssq = x0 + x1;
+      if (g == 0) *reinterpret_cast<float2*>(red + 2 * (wn * 256 + rl)) = make_float2(ssum, ssq);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    {  // thread -> (row, statistic): the 4 column-slices of the 256-column block, in a fixed order
+      const int row = tid >> 1, st = tid & 1;
+      const float v = red[2 * row + st] + red[2 * (256 + row) + st] + red[2 * (512 + row) + st] + red[2 * (768 + row) + st];
+      const int P = (p.N + 255) / 256;
+      const int m = m0 + row;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)e.stats_out, (short)0, (int)((long)p.M * P * 8), 0x00020000);
+      const unsigned vo = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + st) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, vo, 0, 0);
+    }
+    TS(5);
+    return;
+  }
   if (rows_store) {
     // LDS-staged epilogue: phase 1 writes t = gamma * act(acc + bias + rowbias) as fp16 into a
     // [256][OW] image (8-byte units XOR-swizzled by row&15: conflict-free both ways); phase 2 reads
@@ -1324,7 +1514,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
                                                       int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0)];
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0) +
+                                                     (EK == 2 ? 4096 : 0)];
   const int ntiles = tiles_m * tiles_n;
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
     const uint64_t d = (uint64_t)(((blockIdx.x >> 3) % desync) * stagger_ticks / desync);
