@@ -1,5 +1,7 @@
 # Builds the gfx950 kernel library behind the C ABI in include/vda.h.
-#   make            -> video-depth-anything_amd/libvda.so
+#   make            -> video-depth-anything_amd/libvda.so (+ libvda_torch.so)
+#   make tune       -> build/tune/libvda.so (+ libvda_torch.so): the same kernels with -DVDA_TUNING, which
+#                      turns the route knobs into globals set through include/vda_tune.h (tests / tools only)
 #   make oracle     -> nothing to compile (the oracle is a torch-CPU restatement), kept for symmetry
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
@@ -16,12 +18,31 @@ build/vda_attn.o: EXTRA := -fno-honor-nans -mno-amdgpu-ieee
 # GEMM epilogues: SLP packing of scalar f32 math needs register moves that cost more than it saves
 build/vda_gemm.o: EXTRA := -fno-slp-vectorize
 
-build/%.o: $(PKG)/csrc/%.hip $(PKG)/csrc/vda_common.h $(PKG)/csrc/phi_table.h include/vda.h
+build/tune/vda_attn.o: EXTRA := -fno-honor-nans -mno-amdgpu-ieee
+build/tune/vda_gemm.o: EXTRA := -fno-slp-vectorize
+DEPS := $(PKG)/csrc/vda_common.h $(PKG)/csrc/vda_tune.h $(PKG)/csrc/phi_table.h include/vda.h include/vda_tune.h
+
+build/%.o: $(PKG)/csrc/%.hip $(DEPS)
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) $(EXTRA) -c $< -o $@
 
+build/tune/%.o: $(PKG)/csrc/%.hip $(DEPS)
+	@mkdir -p build/tune
+	$(HIPCC) $(CXXFLAGS) $(EXTRA) -DVDA_TUNING -c $< -o $@
+
+# -Bsymbolic: the library's internal calls bind to its own definitions, so the product and the tuning
+# build can be loaded side by side in one process (the tests compare their routes)
 $(PKG)/libvda.so: $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-Bsymbolic $(OBJS) -o $@
+
+TUNE_OBJS := $(patsubst build/%,build/tune/%,$(OBJS))
+build/tune/libvda.so: $(TUNE_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -Wl,-Bsymbolic $(TUNE_OBJS) -o $@
+
+build/tune/libvda_torch.so: build/vda_torch.o build/tune/libvda.so
+	$(CXX) build/vda_torch.o -o $@ $(subst -L $(PKG),-L build/tune,$(TORCH_LDFLAGS))
+
+tune: build/tune/libvda.so build/tune/libvda_torch.so
 
 # torch.ops.vda.* (TORCH_LIBRARY registration over the C ABI): host-only C++ against the installed
 # PyTorch-ROCm headers, linked to libvda.so (found next to it through $$ORIGIN)
@@ -45,4 +66,4 @@ tools/mfma_probe: tools/mfma_probe.hip
 clean:
 	rm -rf build $(PKG)/libvda.so $(PKG)/libvda_torch.so
 
-.PHONY: all clean
+.PHONY: all clean tune

@@ -48,7 +48,7 @@ sys.path.insert(0, REPO)
 PEAK_FP16_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
 REF_A100_FPS = 71.4        # README.md:52-61 ViT-L fp16 14 ms/frame on 1x A100
 GFLOP_PER_FRAME = {("vitl", 518, 518): 1404.6, ("vits", 518, 518): 121.3, ("vitl", 518, 924): 2761.5}
-PROFILE_ROUND = "r02"      # profiles/<round>_pmc_*.json carry the PMC figures quoted in the line
+PROFILE_ROUND = "r03"      # profiles/<round>_pmc_*.json carry the PMC figures quoted in the line
 
 
 def parse():
@@ -340,13 +340,16 @@ def roofline(model, launches):
     M = int(round(flop / (2.0 * 4 * C * C)))
     achieved = flop / (ms * 1e-3) / 1e12
     f1 = pmc("pmc_fc1") or {}
-    mfma_busy = None
-    for name, e in (pmc("pmc_mfma") or {}).get("kernels", {}).items():
-        if "gemm256_kernel<2, 2, false, 1, false, true>" in name:  # fc1: dense, GELU, LayerNorm folded
-            mfma_busy = e.get("mfma_busy")
+    mm = pmc("pmc_mfma") or {}
+    mfma_busy = next((e.get("mfma_busy") for e in mm.get("kernels", {}).values() if e.get("tag") == "enc_fc1"), None)
+    src = lambda name, d: f"profiles/{PROFILE_ROUND}_{name}.json" if d else None
     return {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": f1.get("hbm_bytes_per_launch"),
             "mfma_busy_pmc": mfma_busy,
+            # traffic and mfma_busy_pmc are NOT measured by this run: they are read from the committed
+            # rocprofv3 --pmc summaries named here (tools/pmc_fc1.py, tools/pmc_mfma_summary.py)
+            "pmc_source": {"traffic": src("pmc_fc1", f1), "mfma_busy_pmc": src("pmc_mfma", mfma_busy is not None),
+                           "pmc_tag": "enc_fc1"},
             "kernel": f"gemm256_kernel<2,2,dense,GELU,LN-fold> (encoder norm2 + fc1) M={M} N={4 * C} K={C}",
             "flop_per_launch": flop, "avg_launch_ms": round(ms, 4), "launches": len(rec)}
 

@@ -259,55 +259,9 @@ int vda_depth_head_f32(const float* x, const float* w1, const float* b1, const f
                        const float* b2, float* depth, float* ws_up, float* ws_mid, int32_t BT,
                        int32_t Hin, int32_t Win, int32_t C, int32_t Ho, int32_t Wo, void* stream);
 
-/*
- * Tuning hook: force the GEMM/conv tile configuration (-1 = automatic; 0 = 128x128/4 waves,
- * 1 = 256x128/8 waves, 2 = 128x64/4 waves, 3 = 256x256/8 waves; -2 / -3 = automatic tiles with the
- * strip-tiled 3x3 conv for no / every Cout = 256 shape; 9 = depth tail on a materialised resize
- * instead of the resize fused into the halo conv; 10 + cfg = implicit-GEMM depth tail).
- * Process-global; for benchmarks and tests.
- */
-int vda_debug_force_tile(int32_t cfg);
-
-/*
- * Tuning hook for the phased 256-row GEMM: persist_blocks > 0 launches that many persistent blocks
- * (0 = one block per tile, -1 = automatic: one per CU); stagger_ticks >= 0 forces the start delay
- * (100 MHz ticks) of the delayed half of the blocks, -1 = automatic (none: the drivers run two clips
- * in flight), -2 = half a tile when the last round is short (the one-clip optimum).  Process-global;
- * for tuning.
- */
-int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger);
-/* Tuning hook for the two-blocks-per-CU encoder GEMM (gemm2_kernel): mode -1 = automatic, 0 = never,
- * 1 = every shape it serves; start_ticks = start offset (100 MHz ticks) of the second half of its
- * blocks.  Process-global; for tests and A/B runs. */
-int vda_debug_gemm2(int32_t mode, int32_t start_ticks);
-/* Tuning hook for the spatial attention: 0 = the 4-wave kernel (two blocks per CU), 1 = the 8-wave
- * ping-pong kernel.  Process-global; for tests and A/B runs. */
-int vda_debug_attn(int32_t mode);
-/* Tuning experiment: with groups > 1 every phased-GEMM block starts ((block / 8) % groups) / groups of
- * the stagger ticks late (desynchronises the CUs' epilogue store bursts).  0 = off. */
-int vda_debug_gemm_desync(int32_t groups);
-
-/*
- * Tuning hook for the strip-tiled 3x3 conv: split every tile's input channels over nsplit work items
- * (1, 2, 4, 8; must divide Cin / 32) whose fp32 partials are summed in a fixed order by a finishing
- * kernel (0 = automatic, from a rounds x steps cost model).  Process-global; for tests and tuning.
- */
-int vda_debug_strip_split(int32_t nsplit);
-
-/*
- * Tuning hook for the halo-tiled phased 3x3 conv (Cout = 256, csrc/vda_hconv.hip): -1 = automatic
- * (maps of >= 128^2 pixels), 0 = never (implicit GEMM / strip conv), 1 = every shape it serves.
- * Process-global; for tests and A/B runs.
- */
-int vda_debug_hconv(int32_t mode);
-
-/*
- * Tuning hook for the depth tail (vda_depth_head): -1 = automatic (the 2-blocks-per-CU depth conv of
- * csrc/vda_dconv.hip with the resize fused into its patch building), 2 = the same conv on a
- * materialised resize (bit-identical; needs the workspace), 0 = the older 8-wave halo kernels.  Query
- * vda_depth_head_workspace after changing it.  Process-global.
- */
-int vda_debug_dconv(int32_t mode);
+/* The tuning entry points (vda_debug_*) exist only in the tuning build of the library
+ * (make tune -> build/tune/libvda.so): include/vda_tune.h.  This library keeps no mutable global
+ * state; its kernel routes are the automatic ones. */
 
 #ifdef __cplusplus
 }

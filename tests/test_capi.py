@@ -35,6 +35,27 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_product_library_has_no_tuning_state():
+    """the product libvda.so exports no vda_debug_* hook and holds no writable global
+    besides the per-thread error string and the memoised CU count (a device property); the route
+    knobs exist only in the tuning build (include/vda_tune.h), which exports every hook it declares."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libvda.so not built")
+    dyn = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "vda_debug_" not in dyn
+    syms = subprocess.run(["nm", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    data = [l.split()[-1] for l in syms.splitlines() if re.match(r"\S+ [BbDd] ", l)]
+    data = [d for d in data if not re.search(r"kernel|__hip|fatbin|__dso|_DYNAMIC|_GLOBAL_OFFSET|__do_|__init|__fini", d)]
+    assert sorted(data) == sorted(["_ZN12_GLOBAL__N_15g_errE", "_ZZ12vda_cu_countvE3cus"]), data
+    tune_h = open(os.path.join(REPO, "include", "vda_tune.h")).read()
+    tune_h = re.sub(r"/\*.*?\*/", "", tune_h, flags=re.S)
+    declared = sorted(set(re.findall(r"\b(vda_[a-z0-9_]+)\s*\(", tune_h)))
+    assert declared == sorted(_lib.TUNE_EXPORTED)
+    if os.path.exists(_lib.TUNE_LIB_PATH):
+        tdyn = subprocess.run(["nm", "-D", "--defined-only", _lib.TUNE_LIB_PATH], capture_output=True, text=True).stdout
+        assert set(re.findall(r"\bT (vda_debug_[a-z0-9_]+)", tdyn)) == set(declared)
+
+
 def test_integration_doc_binding_matches_library():
     """INTEGRATION.md's ctypes stub is what a maintainer copies: its Epilogue mirror must have the
     library's sizeof(vda_epilogue) and the field order of _lib.Epilogue (a short struct makes

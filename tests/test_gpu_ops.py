@@ -10,8 +10,9 @@ import torch.nn.functional as F
 
 import vda_amd
 from vda_amd import ops
-from vda_amd._lib import ACT_GELU, ACT_GEGLU, ACT_RELU
+from vda_amd._lib import ACT_GELU, ACT_GEGLU, ACT_RELU, Epilogue
 from vda_amd.model import _geglu_interleave
+from tunelib import tune_lib
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -210,32 +211,6 @@ def test_spatial_attention(B, N, H):
     assert rel(y, ref) < 3e-3
 
 
-@pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1), (1, 257, 2), (2, 2443, 2),
-                                   (1, 130, 1), (1, 1, 1)])
-def test_spatial_attention_pingpong(B, N, H):
-    """The 8-wave ping-pong kernel (two 4-wave groups alternating GEMM and softmax segments over a
-    shared 5-slot K/V ring): bit-identical to the 4-wave kernel (same MFMA and softmax order), and vs
-    torch fp32, for 1 .. 39 key tiles, partial last tiles, a block whose second group is idle (N <=
-    128) and a one-key sequence."""
-    D = 64
-    qkv = rnd(B * N, 3 * H * D, seed=41 + N)
-    # a spike forces the deferred rescale of the running max mid-sequence (rule 26)
-    qkv.view(B, N, 3, H, D)[0, N // 2, 1, 0] *= 40
-    lib = vda_amd._libvda()
-    lib.vda_debug_attn(0)
-    y0 = ops.spatial_attention(h(qkv), B, N, H, D)
-    lib.vda_debug_attn(1)
-    try:
-        y1 = ops.spatial_attention(h(qkv), B, N, H, D)
-    finally:
-        lib.vda_debug_attn(0)
-    q, k, v = qkv.reshape(B, N, 3, H, D).permute(2, 0, 3, 1, 4)
-    ref = ((q @ k.transpose(-1, -2)) * D ** -0.5).softmax(-1) @ v
-    ref = ref.transpose(1, 2).reshape(B * N, H * D)
-    assert rel(y1, ref) < 3e-3
-    assert torch.equal(y0, y1)
-
-
 @pytest.mark.parametrize("B,T,S,D", [(1, 32, 37, 128), (1, 8, 10, 32), (2, 5, 9, 48), (1, 32, 20, 8), (1, 3, 4, 24)])
 def test_temporal_attention(B, T, S, D):
     H = 8
@@ -291,12 +266,10 @@ def test_depth_head_fp32(C, Hin, Win, Ho, Wo, BT):
     # the conv keeps the fp32 weights as hi + lo fp16 halves (22 of 24 mantissa bits) with fp32
     # accumulation: agreement at ~1e-6
     assert rel(y, ref) < 1e-5
-    lib = vda_amd._libvda()
-    lib.vda_debug_force_tile(13)  # the implicit-GEMM depth kernel
-    try:
-        y_old = ops.depth_head(xh, *args)
-    finally:
-        lib.vda_debug_force_tile(-1)
+    T = tune_lib()
+    assert torch.equal(T.depth_head(xh, *args), y)  # the tuning build's automatic route is the product's
+    with T.route(force_tile=13):  # the implicit-GEMM depth kernel
+        y_old = T.depth_head(xh, *args)
     assert rel(y_old, ref) < 1e-5
 
 
@@ -345,11 +318,11 @@ def test_c_abi_direct_matches_torch_ops():
 def test_depth_head_workspace_only_when_used():
     """The op allocates the resized-map workspace exactly when the library's path materialises the
     resize: the default (resize fused into the depth conv of vda_dconv.hip) none, the materialised
-    variant (vda_debug_dconv(2)) one [BT, 518, 518, C] fp16 map (no unused reservation)."""
+    variant (tuning build, vda_debug_dconv(2)) one [BT, 518, 518, C] fp16 map (no unused
+    reservation), and both give the same depth."""
     x = h(rnd(2, 296, 296, 128, scale=0.5, seed=76))
     w1 = h(rnd(64, 3, 3, 128, scale=0.03, seed=77))
     b1, w2, b2 = f32(rnd(32, seed=78)), f32(rnd(32, seed=79)), f32(rnd(1, seed=80))
-    lib = vda_amd._libvda()
 
     def extra_bytes():
         torch.cuda.synchronize()
@@ -363,12 +336,11 @@ def test_depth_head_workspace_only_when_used():
     dmap = 2 * 518 * 518 * 4
     extra, d0 = extra_bytes()  # default: resize fused into the depth conv
     assert extra <= dmap + (4 << 20), extra  # the fp32 depth (+ allocator rounding)
-    lib.vda_debug_dconv(2)
-    try:
-        extra, d1 = extra_bytes()  # materialised resize
-    finally:
-        lib.vda_debug_dconv(-1)
-    assert 2 * 518 * 518 * 128 * 2 <= extra - dmap <= 2 * 518 * 518 * 128 * 2 + (4 << 20), extra
+    assert vda_amd._libvda().vda_depth_head_workspace(2, 296, 296, 128, 518, 518) == 0
+    T = tune_lib()
+    with T.route(dconv=2):  # the same conv on a materialised resize: the library asks for one fp16 map
+        assert T.depth_head_workspace(2, 296, 296, 128, 518, 518) == 2 * 518 * 518 * 128 * 2
+        d1 = T.depth_head(x, w1, b1, w2, b2, 518, 518)
     assert torch.equal(d0, d1)
 
 
@@ -383,12 +355,8 @@ def test_conv3x3_halo_cout128(Cin, H, W, relu):
     xh, wh = h(x.permute(0, 2, 3, 1)), h(w.permute(0, 2, 3, 1))
     y = ops.conv2d(xh, wh, bias=f32(b), act=ACT_RELU if relu else 0)
     assert rel(y, ref) < 2e-3
-    lib = vda_amd._libvda()
-    lib.vda_debug_force_tile(3)
-    try:
-        y2 = ops.conv2d(xh, wh, bias=f32(b), act=ACT_RELU if relu else 0)
-    finally:
-        lib.vda_debug_force_tile(-1)
+    with tune_lib().route(force_tile=3) as T:
+        y2 = T.conv2d(xh, wh, bias=f32(b), act=ACT_RELU if relu else 0)
     assert rel(y, y2) < 1e-3
 
 
@@ -417,7 +385,8 @@ def test_conv3x3_strip_cout256(Cin, H, W, BT, mode):
     """3x3 convs with 256 outputs on maps <= 160 wide on the strip-tiled halo kernel (layerN_rn,
     blocks.py:20-32; RCU conv1 with pre-ReLU + ReLU, conv2 with the skip and fusion adds,
     blocks.py:78-91 / :146-150); partial last tiles, tiles spanning 3 rows, Cin = 32 .. 1024.
-    vs torch fp32 and vs the implicit-GEMM conv (vda_debug_force_tile(-2))."""
+    vs torch fp32 and vs the implicit-GEMM conv (tuning build: vda_debug_force_tile(-3) takes the strip
+    kernel for every Cin, the default only for Cin >= 512 or under-filled grids; -2 never)."""
     x = rnd(BT, Cin, H, W, seed=90)
     w, b = rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=91), rnd(256, scale=0.1, seed=92)
     r1, r2 = rnd(BT, 256, H, W, seed=93), rnd(BT, 256, H, W, seed=94)
@@ -433,18 +402,14 @@ def test_conv3x3_strip_cout256(Cin, H, W, BT, mode):
         kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
     ref = ref.permute(0, 2, 3, 1)
     xh, wh = nh(x), nh(w)
-    lib = vda_amd._libvda()
-    lib.vda_debug_force_tile(-3)  # strip kernel for every Cin (the default takes it for Cin >= 512)
-    try:
-        y = ops.conv2d(xh, wh, **kw)
-    finally:
-        lib.vda_debug_force_tile(-1)
+    T = tune_lib()
+    y0 = ops.conv2d(xh, wh, **kw)  # the product's route
+    assert rel(y0, ref) < 2e-3
+    with T.route(force_tile=-3):  # strip kernel for every Cin
+        y = T.conv2d(xh, wh, **kw)
     assert rel(y, ref) < 2e-3
-    lib.vda_debug_force_tile(-2)
-    try:
-        y2 = ops.conv2d(xh, wh, **kw)
-    finally:
-        lib.vda_debug_force_tile(-1)
+    with T.route(force_tile=-2):
+        y2 = T.conv2d(xh, wh, **kw)
     assert rel(y, y2) < 1e-3
 
 
@@ -471,17 +436,12 @@ def test_conv3x3_strip_split(Cin, H, W, BT, mode, split):
         kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
     ref = ref.permute(0, 2, 3, 1)
     xh, wh = nh(x), nh(w)
-    lib = vda_amd._libvda()
-    lib.vda_debug_force_tile(-3)
-    try:
-        lib.vda_debug_strip_split(split)
-        y = ops.conv2d(xh, wh, **kw)
-        y_again = ops.conv2d(xh, wh, **kw)
-        lib.vda_debug_strip_split(1)
-        y1 = ops.conv2d(xh, wh, **kw)
-    finally:
-        lib.vda_debug_strip_split(0)
-        lib.vda_debug_force_tile(-1)
+    T = tune_lib()
+    with T.route(force_tile=-3, strip_split=split):
+        y = T.conv2d(xh, wh, **kw)
+        y_again = T.conv2d(xh, wh, **kw)
+    with T.route(force_tile=-3, strip_split=1):
+        y1 = T.conv2d(xh, wh, **kw)
     assert torch.equal(y, y_again)
     assert rel(y, ref) < 2e-3
     assert rel(y, y1) < 1e-3
@@ -491,8 +451,9 @@ def test_conv3x3_strip_split(Cin, H, W, BT, mode, split):
                                                  (64, 30, 17, 53, 31, 2), (128, 12, 12, 12, 12, 1), (64, 5, 40, 33, 47, 1)])
 def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
     """Depth tail with the bilinear resize fused into the patch building of the depth conv (default):
-    bit-identical to the materialised resize + the same conv (vda_debug_dconv(2)); and the older
-    fused 8-wave halo conv (vda_debug_dconv(0)) bit-identical to the materialised resize + halo conv (vda_debug_force_tile(9)),
+    bit-identical to the materialised resize + the same conv (tuning build: vda_debug_dconv(2)); and the
+    older fused 8-wave halo conv (vda_debug_dconv(0)) bit-identical to the materialised resize + halo conv
+    (vda_debug_force_tile(9)),
     both interpolating with the same fp32 formula and fp16 rounding; partial tiles, non-square maps,
     identity-size resize, aspect ratios far from 1."""
     x = rnd(BT, C, Hin, Win, seed=145)
@@ -506,23 +467,14 @@ def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
     split = torch.cat([wn.half(), (wn - wn.half().float()).half()], 0).to(DEV).contiguous()
     args = (split, f32(b1), f32(w2.reshape(-1)), f32(b2), Ho, Wo)
     y = ops.depth_head(xh, *args)  # default: the 2-blocks-per-CU depth conv, resize fused into its patches
-    lib = vda_amd._libvda()
-    lib.vda_debug_dconv(2)  # the same conv on a materialised resize
-    try:
-        y_mat2 = ops.depth_head(xh, *args)
-    finally:
-        lib.vda_debug_dconv(-1)
+    T = tune_lib()
+    with T.route(dconv=2):  # the same conv on a materialised resize
+        y_mat2 = T.depth_head(xh, *args)
     assert torch.equal(y, y_mat2)
-    lib.vda_debug_dconv(0)
-    try:
-        y_fused = ops.depth_head(xh, *args)
-    finally:
-        lib.vda_debug_dconv(-1)
-    lib.vda_debug_force_tile(9)
-    try:
-        y_mat = ops.depth_head(xh, *args)
-    finally:
-        lib.vda_debug_force_tile(-1)
+    with T.route(dconv=0):
+        y_fused = T.depth_head(xh, *args)
+    with T.route(force_tile=9):
+        y_mat = T.depth_head(xh, *args)
     assert torch.equal(y_fused, y_mat)  # the older 8-wave halo kernels, fused vs materialised
     assert rel(y_fused, ref) < 1e-5
     assert rel(y, ref) < 1e-5
@@ -607,22 +559,14 @@ def test_conv3x3_hconv_cout256(Cin, H, W, BT, mode):
         kw = dict(bias=f32(b), res=nh(r1), res2=nh(r2))
     ref = ref.permute(0, 2, 3, 1)
     xh, wh = nh(x), nh(w)
-    lib = vda_amd._libvda()
-    lib.vda_debug_hconv(1)
-    try:
-        y = ops.conv2d(xh, wh, **kw)
-        y_again = ops.conv2d(xh, wh, **kw)
-    finally:
-        lib.vda_debug_hconv(-1)
+    T = tune_lib()
+    with T.route(hconv=1):
+        y = T.conv2d(xh, wh, **kw)
+        y_again = T.conv2d(xh, wh, **kw)
     assert rel(y, ref) < 2e-3
     assert torch.equal(y, y_again)
-    lib.vda_debug_hconv(0)
-    lib.vda_debug_force_tile(-2)
-    try:
-        y2 = ops.conv2d(xh, wh, **kw)
-    finally:
-        lib.vda_debug_force_tile(-1)
-        lib.vda_debug_hconv(-1)
+    with T.route(hconv=0, force_tile=-2):
+        y2 = T.conv2d(xh, wh, **kw)
     assert rel(y, y2) < 1e-3
 
 
@@ -659,3 +603,13 @@ def test_gemm_epilogue_row_stats(M, N, K):
     yb = ops.gemm(tok, wg.to(DEV), bias=bb, ln_stats=ops.row_stats(tok, 1e-6), ln_colsum=c1)
     ref = F.linear(F.layer_norm(y, (N,), gam, bet, eps=1e-6), w2)
     assert rel(ya, ref) < 2e-3 and rel(ya, yb) < 1e-3
+    # the register residual epilogue of the tuning build (vda_debug_gemm_epi(1), EK 2 for the phased
+    # shapes): bit-identical outputs; the statistics sum in another order
+    tok2, st2 = r.to(DEV).contiguous(), torch.full((M + 1, P, 2), float("nan"), device=DEV)
+    xh, wh, bf = h(x), h(w), f32(b)
+    e = Epilogue(rdiv=1, rmod=1, bias=bf.data_ptr(), res=tok2.data_ptr(), ldres=N, stats_out=st2.data_ptr())
+    with tune_lib().route(gemm_epi=1) as T:
+        T.gemm(xh, wh, tok2, e, M, N, K)
+    torch.cuda.synchronize()
+    assert torch.equal(tok2, tok)
+    assert torch.allclose(st2[:M], st[:M], rtol=1e-5, atol=1e-4)

@@ -1,8 +1,6 @@
 """In-process A/B of the encoder GEMMs across libvda builds (tuning tool, not product code).
 
-usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so[@g2=TICKS] ...] [--rounds R] [--shapes qkv,proj,fc1,fc2]
-(LIB@g2=TICKS: that library with the two-blocks-per-CU kernel forced, second-half start offset TICKS;
-give each variant its own copy of the .so, since the tuning hooks are library-global)
+usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes qkv,proj,fc1,fc2]
 
 Each library is loaded through ctypes and called through the C ABI (vda_gemm) on the current torch
 stream with the forward's exact epilogues (LN fold from [M, 4, 2] partials for qkv / fc1, residual +
@@ -34,10 +32,6 @@ for k, p in enumerate(libs):
     path, _, opt = p.partition("@")
     l = ctypes.CDLL(os.path.abspath(path))
     _lib._declare(l)
-    if opt.startswith("g2="):
-        l.vda_debug_gemm2(1, int(opt[3:]))
-    elif opt.startswith("g2m2="):  # one block per CU
-        l.vda_debug_gemm2(2, int(opt[5:]))
     L.append(l)
 
 dev = "cuda"

@@ -1,10 +1,13 @@
 """Spatial-attention microbenchmark at the ViT-L clip shape (32 frames x 1370 tokens x 16 heads x 64):
-us per call, TFLOP/s (4·B·H·N²·D), and rel error vs torch SDPA on the same fp16 inputs."""
+us per call, TFLOP/s (4·B·H·N²·D), and rel error vs torch SDPA on the same fp16 inputs.  With VDA_LIB_OVERRIDE=build/tune/libvda.so and
+VDA_ATTN_OLD=1 the round-1 kernel (vda_debug_attn)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn.functional as F
-from vda_amd import ops
+from vda_amd import ops, _lib
+if os.environ.get("VDA_ATTN_OLD"):
+    _lib.lib().vda_debug_attn(1, 0)
 
 B, N, H, D = 32, 1370, 16, 64
 torch.manual_seed(0)

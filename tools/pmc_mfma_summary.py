@@ -11,6 +11,30 @@ the guide notes it reads high on dispatches shorter than ~0.3 ms."""
 import csv, json, re, sys
 from collections import defaultdict
 
+# Stable tags of the forward's kernel classes (the demangled names carry template arguments that change
+# as kernels evolve; bench.py looks its figures up by tag).  Template arguments of gemm256_kernel:
+# <XR, WR, CONV, ACT, ROWB, LNF, EK>; ACT 1 = GELU; LNF = LayerNorm folded into the epilogue.
+TAGS = [
+    (r"^gemm256_kernel<2, 2, false, 1, false, true\b", "enc_fc1"),        # norm2 + fc1 + GELU
+    (r"^gemm256_kernel<2, 2, false, 0, false, true\b", "enc_qkv"),        # norm1 + qkv
+    (r"^gemm256_kernel<2, 2, false, 0, false, false\b", "enc_proj_fc2"),  # proj / fc2 + residual + row stats
+    (r"^gemm256_kernel<2, 2, true\b", "conv_phased"),
+    (r"^spatial_attn32_kernel", "spatial_attention"),
+    (r"^temporal_attn_lds_kernel", "temporal_attention"),
+    (r"^depth_conv_kernel", "depth_conv"),
+    (r"^halo_conv_kernel<64, 128, 1", "output_conv1"),
+    (r"^hconv_kernel|^halo256", "conv3x3_halo256"),
+    (r"^strip_conv", "conv3x3_strip"),
+]
+
+
+def tag_of(name):
+    for rx, t in TAGS:
+        if re.search(rx, name):
+            return t
+    return None
+
+
 path, out = sys.argv[1], sys.argv[2]
 n_cu = int(sys.argv[3]) if len(sys.argv) > 3 else 256
 disp = defaultdict(dict)
@@ -34,7 +58,7 @@ res = {"n_cu": n_cu, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 *
 tot_b = tot_c = 0.0
 for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["kernel_cycles"]):
     busy = a["mfma_busy_cycles"] / max(1.0, a["kernel_cycles"] * n_cu * 4)
-    e = {"dispatches": a["dispatches"], "mfma_busy": round(busy, 4), "kernel_cycles": a["kernel_cycles"]}
+    e = {"tag": tag_of(k), "dispatches": a["dispatches"], "mfma_busy": round(busy, 4), "kernel_cycles": a["kernel_cycles"]}
     if a["ns"]:
         e["clock_ghz"] = round(a["kernel_cycles"] / a["ns"], 3)
     res["kernels"][k] = e

@@ -26,9 +26,11 @@ EXPORTED = (
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
     "vda_temporal_attention_f32", "vda_upsample_bilinear_f32", "vda_patch_im2col_f32", "vda_depth_head_f32",
-    "vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_gemm2", "vda_debug_attn", "vda_debug_strip_split",
-    "vda_debug_hconv", "vda_debug_dconv",
 )
+# The tuning build (make tune -> build/tune/libvda.so, include/vda_tune.h) adds these.
+TUNE_EXPORTED = ("vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_gemm_epi",
+                 "vda_debug_strip_split", "vda_debug_hconv", "vda_debug_dconv", "vda_debug_attn")
+TUNE_LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "tune", "libvda.so")
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
 STORE_ROWS, STORE_PIXEL_SHUFFLE = 0, 1
@@ -92,15 +94,15 @@ def _declare(lib):
         "vda_debug_force_tile": ([I], I),
         "vda_debug_gemm_sched": ([I, I], I),
         "vda_debug_gemm_desync": ([I], I),
-        "vda_debug_gemm2": ([I, I], I),
-        "vda_debug_attn": ([I], I),
         "vda_debug_strip_split": ([I], I),
         "vda_debug_hconv": ([I], I),
         "vda_debug_dconv": ([I], I),
+        "vda_debug_gemm_epi": ([I], I),
+        "vda_debug_attn": ([I, I], I),
     }
     for name, (args, res) in sig.items():
         if name.startswith("vda_debug_") and not hasattr(lib, name):
-            continue  # tuning hooks may be absent from an older library under A/B comparison
+            continue  # tuning hooks: only in the tuning build
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = res
@@ -122,10 +124,6 @@ def lib():
         if l.vda_epilogue_size() != ctypes.sizeof(Epilogue):  # the ctypes mirror must match include/vda.h
             raise OSError(f"vda_epilogue is {l.vda_epilogue_size()} bytes in the library, {ctypes.sizeof(Epilogue)} "
                           f"in _lib.Epilogue: rebuild libvda.so or update the mirror")
-        sched = os.environ.get("VDA_GEMM_SCHED")  # tuning: "persist_blocks,stagger_ticks"
-        if sched and hasattr(l, "vda_debug_gemm_sched"):
-            pb, st = (int(v) for v in sched.split(","))
-            l.vda_debug_gemm_sched(pb, st)
     except OSError as e:  # pragma: no cover - depends on the runtime
         _load_error = f"failed to load {LIB_PATH}: {e}"
         raise VDAUnavailable(_load_error) from e

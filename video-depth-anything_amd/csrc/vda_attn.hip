@@ -384,218 +384,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
 }
 
 // =============================================================================================
-// Spatial attention v3, D = 64: two 4-wave groups per block in ping-pong (the two-waves-per-SIMD
-// schedule of MI355X_MICROARCH.md).  At d = 64 a 64-key tile costs a wave 16 MFMAs (512 cycles)
-// but ~600 cycles of softmax VALU, so one wave cannot keep its matrix pipe busy; v2 relied on two
-// unrelated blocks per CU happening to be out of phase.  Here a block holds 8 waves (256 queries of
-// one (b, h)): group A = waves 0-3, group B = waves 4-7, so every SIMD hosts one wave of each, and
-// the block runs in lockstep segments separated by one s_barrier each:
-//   segment s: the group whose turn it is runs its GEMM phase   PV(t-1) + QK(t)   (16 MFMAs)
-//              the other group runs its softmax phase of tile t (max, exp2, row sum, P to fp16,
-//              rescale) and prefetches the fragments of its next GEMM phase: K(t+1) and V(t)
-// The groups alternate each segment, so each softmax runs beside the partner's MFMAs.  K/V tiles
-// (8 KiB each) share one 4-slot LDS ring (both groups walk the same keys, one segment apart);
-// tile u is DMA'd four segments before its first read.  Scores, P and O layouts are v2's.
-// =============================================================================================
-constexpr int PP_QB = 256;   // queries per block (two groups of 128)
-constexpr int PP_NBUF = 5;   // K/V ring depth
-
-__global__ __launch_bounds__(512, 2) void spatial_attn_pp_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                                 int N, int H, int nqb, int nblocks, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) h16 sKV[PP_NBUF][2][SA_KT * SD];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int gi = wave >> 2;  // 0: group A, 1: group B
-  int id = blockIdx.x;
-  const int per = nblocks >> 3;
-  if (id < per * 8) id = (id & 7) * per + (id >> 3);  // all query blocks of one (b, h) on one XCD
-  const int qb = __builtin_amdgcn_readfirstlane(id % nqb), bh = id / nqb;
-  const int h = __builtin_amdgcn_readfirstlane(bh % H), b = __builtin_amdgcn_readfirstlane(bh / H);
-  const int C = H * SD;
-  const long ld = 3L * C;
-  const h16* base = qkv + (long)b * N * ld + h * SD;
-  const int r32 = lane & 31, hf = lane >> 5;
-  const int q = qb * PP_QB + gi * 128 + (wave & 3) * 32 + r32;
-
-  h8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    h8 t = h8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (q < N) t = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + ks * 16 + hf * 8));
-#pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = (h16)((float)t[e] * scale_log2);
-    qf[ks] = t;
-  }
-
-  // 16 pieces per tile (8 K + 8 V, 8 key rows each); wave w moves pieces 2w, 2w + 1
-  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
-  unsigned voff[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int gp = wave * 2 + j, isv = gp >> 3, pc = gp & 7;
-    const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
-    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
-    voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
-  }
-  auto dma = [&](int kt) {
-    const int buf = kt % PP_NBUF;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int gp = wave * 2 + j, isv = gp >> 3, pc = gp & 7;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
-                                               (int)(kt * SA_KT * ld * 2), 0, 0);
-    }
-  };
-
-  f16x o[2] = {f16x{}, f16x{}};
-  f16x negm = {};
-  f16x s[2];
-  float mrun = 0.f, lsum = 0.f;
-  h8 pf[4], kf[8], vf[8];
-  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  const int nt = (N + SA_KT - 1) / SA_KT;
-  const bool tail = N % SA_KT != 0;
-
-  // per-lane LDS offsets (halfs) inside a ring slot: the K swizzle depends on (r32, ks) only (kb adds
-  // 32 rows), the V swizzle on (q4, dt) only (ps adds 16 rows, the second read 8 rows); the slot is a
-  // wave-uniform offset, so every fragment read is base + immediate
-  int kofs[4], vofs[2];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kofs[ks] = sa_kslot(r32, ks * 2 + hf) * 8;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int col = dt * 32 + (grp & 1) * 16 + 4 * p4;
-    const int r0 = 4 * (grp >> 1) + q4;
-    vofs[dt] = SA_KT * SD + sa_vslot(r0, col >> 3) * 8 + (col & 7);
-  }
-  const h16* ring = &sKV[0][0][0];
-  auto slot_base = [&](int kt) { return ring + __builtin_amdgcn_readfirstlane((kt % PP_NBUF) * (2 * SA_KT * SD)); };
-  auto read_k = [&](int kt) {  // K(kt) fragments of the next QK
-    const h16* sk = slot_base(kt);
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) kf[kb * 4 + ks] = *reinterpret_cast<const h8*>(sk + kofs[ks] + kb * 32 * 64);
-  };
-  auto read_v = [&](int kt) {  // V(kt)ᵀ fragments of the next PV (same permuted key order as v2)
-    const h16* sv = slot_base(kt);
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        const h4 v0 = lds_read_tr16(sv + vofs[dt] + ps * 16 * 64);
-        const h4 v1 = lds_read_tr16(sv + vofs[dt] + ps * 16 * 64 + 8 * 64);
-        vf[dt * 4 + ps] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-      }
-  };
-  auto gemm = [&](int t) {  // GEMM phase of tile t: QK(t) from the prefetched kf, then PV(t-1) (V read here)
-    __builtin_amdgcn_s_setprio(1);
-    if (t < nt) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) s[kb] = mfma32(kf[kb * 4 + ks], qf[ks], ks == 0 ? negm : s[kb]);
-    }
-    if (t >= 1) {
-      read_v(t - 1);
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int ps = 0; ps < 4; ++ps) o[dt] = mfma32(vf[dt * 4 + ps], pf[ps], o[dt]);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // one body for every tile (separate first / masked instantiations of it quadruple the register
-  // pressure across the loop: 256 VGPRs + spills instead of ~175)
-  auto softmax = [&](int kt, bool FIRST, bool MASK) {
-    if (MASK) {  // keys >= N of the last tile; lim laundered so the 32 compares stay here
-      int lim = N - kt * SA_KT - 4 * hf;
-      asm volatile("" : "+v"(lim));
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kb * 32 + (r & 3) + 8 * (r >> 2) >= lim) s[kb][r] = -INFINITY;
-    }
-    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
-    mx = fmaxf(fmaxf(mx, s[0][15]), s[1][0]);
-#pragma unroll
-    for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
-    mx = fmaxf(mx, s[1][15]);
-    mx = half_max(mx);
-    if (FIRST || __any(mx > 8.f)) {  // deferred rescale (v2): re-base only when P could exceed 2^8
-      const float sh = FIRST ? mx : fmaxf(mx, 0.f);
-      mrun += sh;
-      if (!FIRST) {
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-        lsum *= alpha;
-        o[0] *= alpha;
-        o[1] *= alpha;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) negm[r] = -mrun;
-      s[0] -= sh;
-      s[1] -= sh;
-    }
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(s[kb][r]);
-        lsum += p;
-        pf[kb * 2 + (r >> 3)][r & 7] = (h16)p;
-      }
-  };
-
-  // Every wave runs the same loop of local segments: 2t = GEMM(t) [QK(t), PV(t-1)], 2t+1 = softmax(t)
-  // [+ prefetch K(t+1)]; group B runs one barrier behind group A, so B's GEMM shares a segment with
-  // A's softmax and vice versa.  Tile u (ring slot u % 5): DMA at local segment 2u-6, awaited
-  // (vmcnt) at the end of local segment 2u-3; the slot's previous tile u-5 was last read (V, by B's
-  // GEMM) in global segment 2u-7.
-  auto softmax_t = [&](int t) { softmax(t, t == 0, tail && t == nt - 1); };
-  const int npre = nt < 3 ? nt : 3;
-  for (int u = 0; u < npre; ++u) dma(u);
-  if (npre == 3) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // tiles 0, 1 landed; 2 in flight
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  read_k(0);
-  if (gi) __builtin_amdgcn_s_barrier();  // group B: one segment behind
-  for (int t = 0; t <= nt; ++t) {
-    if (t + 3 < nt) dma(t + 3);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // prefetched K fragments in registers
-    gemm(t);
-    __builtin_amdgcn_s_barrier();
-    if (t < nt) {
-      softmax_t(t);
-      if (t + 1 < nt) read_k(t + 1);
-      if (t + 2 < nt) {  // tile t+2 landed (tile t+3 may stay in flight)
-        if (t + 3 < nt) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // every fragment read of the ring done before the barrier
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-  if (!gi) __builtin_amdgcn_s_barrier();  // balance the stagger
-  // epilogue: lane holds Oᵀ[d = dt*32 + 8gq + 4hf + r][q]
-  const float inv = 1.f / half_sum(lsum);
-  if (q < N) {
-    h16* op = out + ((long)b * N + q) * C + h * SD;
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-      for (int gq = 0; gq < 4; ++gq) {
-        h4 v;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (h16)(o[dt][gq * 4 + r] * inv);
-        *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
-      }
-  }
-}
-
-// =============================================================================================
 // Temporal attention: one wave per (batch, site s, head), T <= 32 frames, v_mfma_f32_32x32x16_f16.
 //   Sᵀ[key][q] = Σ_d K[key][d] Q[q][d]       A = K rows, B = Q rows (fragments straight from HBM)
 //   Oᵀ[d][q]   = Σ_key Vᵀ[d][key] Pᵀ[key][q]  B = Pᵀ accumulator registers 8s..8s+7 (k order
@@ -844,27 +632,26 @@ __global__ __launch_bounds__(64 * NW) void temporal_attn_lds_kernel(const h16* _
   }
 }
 
+// vda_debug_attn (tuning build): the round-1 spatial kernel / the direct-load temporal kernel
+VDA_KNOB(int, g_sa_old, 0);
+VDA_KNOB(int, g_ta_old, 0);
+
 }  // namespace
 
-int g_attn_mode = 0;  // spatial attention kernel: 0 = v2 (spatial_attn32_kernel), 1 = ping-pong (A/B)
-extern "C" int vda_debug_attn(int32_t mode) {
-  g_attn_mode = mode;
+#ifdef VDA_TUNING
+extern "C" int vda_debug_attn(int32_t spatial_old, int32_t temporal_old) {
+  g_sa_old = spatial_old;
+  g_ta_old = temporal_old;
   return 0;
 }
+#endif
 
 extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int32_t N, int32_t H,
                                      int32_t D, float scale, void* stream) {
   VDA_CHECK_ARG(qkv && out, "null pointer");
   VDA_CHECK_ARG(B > 0 && N > 0 && H > 0, "empty attention");
   VDA_CHECK_ARG(D == SD, "spatial attention supports head dim 64 only");
-  static const bool old_kernel = getenv("VDA_ATTN_OLD") != nullptr;  // A/B only
-  if (g_attn_mode == 1) {
-    const int nqb = (N + PP_QB - 1) / PP_QB;
-    const long nb = (long)nqb * H * B;
-    VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
-    hipLaunchKernelGGL(spatial_attn_pp_kernel, dim3((unsigned)nb), dim3(512), 0, (hipStream_t)stream, (const h16*)qkv,
-                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
-  } else if (old_kernel) {
+  if (g_sa_old) {
     dim3 grid((N + SQB - 1) / SQB, H, B);
     hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, scale * 1.4426950408889634f);
@@ -890,9 +677,8 @@ extern "C" int vda_temporal_attention(const void* qkv, void* out, int32_t B, int
   hipStream_t st = (hipStream_t)stream;
   const float sl = scale * 1.4426950408889634f;
   // q / k / v rows staged in LDS for the head dims the model uses (128 at C = 1024, 32 at C = 256, 8
-  // heads); VDA_TA_OLD selects the direct-load kernel (A/B only)
-  static const bool ta_old = getenv("VDA_TA_OLD") != nullptr;
-  if (!ta_old && (D == 32 || D == 64 || D == 128)) {
+  // heads); the direct-load kernel below serves the other head dims
+  if (!g_ta_old && (D == 32 || D == 64 || D == 128)) {
     const int nw = D == 128 ? 2 : 4;  // 24 / 12 / 6 KiB of LDS per wave
     if (H % nw == 0) {
       const unsigned g = (unsigned)((items + nw - 1) / nw);

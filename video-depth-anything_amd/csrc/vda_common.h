@@ -7,6 +7,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "vda_tune.h"
 
 typedef _Float16 h16;
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -157,6 +158,10 @@ __device__ __forceinline__ h8 relu8(h8 x) {
   return __builtin_bit_cast(h8, __builtin_elementwise_max(__builtin_bit_cast(s8v, x), s8v{0, 0, 0, 0, 0, 0, 0, 0}));
 }
 __device__ __forceinline__ uint4 relu_h8(uint4 v) { return __builtin_bit_cast(uint4, relu8(__builtin_bit_cast(h8, v))); }
+
+// Compute units of the current device (hipDeviceAttributeMultiprocessorCount), memoised per device:
+// a read-only device property, not tuning state (vda_misc.hip).
+int vda_cu_count();
 
 // Error reporting across the C ABI (never throws).
 int vda_set_error(int code, const char* msg);

@@ -367,11 +367,10 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
   }
 }
 
-int g_dc_cus = 0;
-
 }  // namespace
 
-int g_dconv_mode = -1;  // vda_debug_dconv: -1 automatic (fused), 0 never, 2 resize + unfused depth conv
+// vda_debug_dconv (tuning build): -1 automatic (fused), 0 never, 2 resize + unfused depth conv
+VDA_KNOB(int, g_dconv_mode, -1);
 
 bool vda_depth_conv_serves(int H, int W, int C) { return C % 32 == 0 && C > 0 && H > 0 && W > 0 && g_dconv_mode != 0; }
 
@@ -379,17 +378,12 @@ bool vda_depth_conv_serves(int H, int W, int C) { return C % 32 == 0 && C > 0 &&
 int vda_depth_conv(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
                    int BT, int H, int W, int C, hipStream_t st) {
   if (!vda_depth_conv_serves(H, W, C)) return 1;
-  if (g_dc_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_dc_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DC_T - 1) / DC_T, tiles_y = (H + DC_T - 1) / DC_T;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL / 9 / ((C + 31) / 32)) return vda_set_error(-22, "depth conv: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < 2 * g_dc_cus ? ntiles : 2 * g_dc_cus;
+  const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
   hipLaunchKernelGGL(depth_conv_kernel<false>, dim3(grid), dim3(256), 0, st, (const h16*)U, (const h16*)w1, b1, w2, b2,
                      depth, H, W, C, tiles_x, tiles_y, ntiles, H, W);
   VDA_LAUNCH_CHECK();
@@ -408,24 +402,21 @@ bool vda_depth_conv_fused_serves(int Hs, int Ws, int H, int W, int C) {
 int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                          float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st) {
   if (!vda_depth_conv_fused_serves(Hs, Ws, H, W, C)) return 1;
-  if (g_dc_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_dc_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DC_T - 1) / DC_T, tiles_y = (H + DC_T - 1) / DC_T;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL / 9 / ((C + 31) / 32)) return vda_set_error(-22, "depth conv: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < 2 * g_dc_cus ? ntiles : 2 * g_dc_cus;
+  const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
   hipLaunchKernelGGL(depth_conv_kernel<true>, dim3(grid), dim3(256), 0, st, (const h16*)x, (const h16*)w1, b1, w2, b2,
                      depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws);
   VDA_LAUNCH_CHECK();
   return 0;
 }
 
+#ifdef VDA_TUNING
 extern "C" int vda_debug_dconv(int32_t mode) {
   g_dconv_mode = mode;
   return 0;
 }
+#endif

@@ -341,8 +341,6 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   }
 }
 
-int g_num_cus = 0;
-
 }  // namespace
 
 // called by vda_depth_head (vda_gemm.hip) after the resize into ws; returns 1 if the shape is not
@@ -350,17 +348,12 @@ int g_num_cus = 0;
 int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
                    int BT, int H, int W, int C, hipStream_t st) {
   if (!(C == 32 || C % 64 == 0)) return 1;
-  if (g_num_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_num_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL) return vda_set_error(-22, "depth head: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  const int grid = ntiles < cus ? ntiles : cus;
   if (C == 32)
     hipLaunchKernelGGL((halo_conv_kernel<32, 64, 3, true>), dim3(grid), dim3(512), 0, st, (const h16*)U, (const h16*)w1,
                        b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles);
@@ -384,17 +377,12 @@ bool vda_depth_halo_fused_serves(int Hs, int Ws, int H, int W, int C) {
 int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const float* w2, const float* b2,
                          float* depth, int BT, int Hs, int Ws, int H, int W, int C, hipStream_t st) {
   if (!vda_depth_halo_fused_serves(Hs, Ws, H, W, C)) return 1;
-  if (g_num_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_num_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL) return vda_set_error(-22, "depth head: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  const int grid = ntiles < cus ? ntiles : cus;
   hipLaunchKernelGGL((halo_conv_kernel<64, 64, 3, true, true>), dim3(grid), dim3(512), 0, st, (const h16*)x,
                      (const h16*)w1, b1, w2, b2, depth, (h16*)nullptr, 0, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws);
   VDA_LAUNCH_CHECK();
@@ -409,17 +397,12 @@ int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias
   if (Cout != 128 || Cin % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return 1;
   const float sy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f, sx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
   if (((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) > 192) return 1;
-  if (g_num_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_num_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  const int grid = ntiles < cus ? ntiles : cus;
   hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false, true>), dim3(grid), dim3(512), 0, st, (const h16*)x,
                      (const h16*)w, bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu,
                      H, W, Cin, tiles_x, tiles_y, ntiles, Hs, Ws);
@@ -433,17 +416,12 @@ int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias
 int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
                   int Cout, hipStream_t st) {
   if (Cout != 128 || Cin % 64 != 0) return 1;
-  if (g_num_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_num_cus = n > 0 ? n : 256;
-  }
+  const int cus = vda_cu_count();
   const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
   const long nt = (long)BT * tiles_x * tiles_y;
   if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
   const int ntiles = (int)nt;
-  const int grid = ntiles < g_num_cus ? ntiles : g_num_cus;
+  const int grid = ntiles < cus ? ntiles : cus;
   hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false>), dim3(grid), dim3(512), 0, st, (const h16*)x, (const h16*)w,
                      bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu, H, W, Cin,
                      tiles_x, tiles_y, ntiles);

@@ -1545,334 +1545,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   }
 }
 
-// ---- two 4-wave blocks per CU (dense encoder GEMMs) ------------------------------------------
-// The phased 256x256 kernel above spends ~25-30 % of every tile outside its main loop with the
-// matrix cores idle: the LN-fold / GELU epilogue (LDS-bound table reads, ~7.6 us per fc1 tile),
-// the output stores and the next prologue (profiles/r03_ts_probe.log).  Here a CU holds TWO
-// independent 256-thread blocks of 80 KiB LDS each: while one block runs its epilogue (VALU + LDS +
-// stores), the other block's main loop owns the matrix cores, so the epilogue costs wall time only
-// where both blocks sit in theirs.
-//   tile 128 (m, X rows) x 256 (n, W rows), BK = 32, three K stages of 24 KiB in LDS (72 KiB) +
-//   the 1,024-line Phi table (8 KiB) for GELU; 4 waves as 2 (m) x 2 (n), wave tile 64 x 128
-//   (acc[8][4]: lane = 4 consecutive channels of one row, as in every kernel of this file).
-//   Stage s + 2 is issued by LDS-DMA right after the barrier that retires stage s (counted vmcnt,
-//   raw s_barrier); fragments by ds_read_b128 from 64-B rows whose 16-B chunk is XOR-swizzled by
-//   g[(row >> 2) & 3], g = {0, 2, 3, 1} (conflict-free for the 4 lane groups of ds_read_b128).
-//   Epilogue operands (bias, LN colsum, the rows' LN partials) are read from L2 when the main loop
-//   ends; the output tile is staged through LDS and leaves as whole 512-B rows, the next tile's
-//   first two stages are issued before those stores (chained prologue, as gemm256_tile).
-namespace g2 {
-constexpr int BM = 128, BN = 256, BKS = 32, NS = 3;
-constexpr int STG = (BM + BN) * BKS;        // halfs per K stage (24 KiB)
-constexpr int PHI_HALVES = 4096;            // the 1,024-line table (8 KiB)
-constexpr int NIT = 16;                     // output stores per lane
-constexpr float PHI1K_MAGIC = 12583424.f;   // 1.5 * 2^23 + 512: round(64 x) + 512
-constexpr float PHI1K_LO = 12582912.f, PHI1K_HI = 12583935.f;
-__device__ __forceinline__ int chunk_swz(int row, int chunk) { return chunk ^ ((0x78 >> (((row >> 2) & 3) * 2)) & 3); }
-__device__ __forceinline__ float gelu_tab1k(float x, unsigned phib) {
-  const float v = __builtin_amdgcn_fmed3f(fmaf(x, 64.f, PHI1K_MAGIC), PHI1K_LO, PHI1K_HI);
-  const phi_f2 ab = *(lds_cf2p)(uintptr_t)((__builtin_bit_cast(unsigned, v) << 3) + phib);
-  return x * fmaf(x, ab.y, ab.x);
-}
-}  // namespace g2
+// Knobs of the tuning build (include/vda_tune.h); compile-time constants in the product library.
+VDA_KNOB(int, g_force_tile, -1);  // vda_debug_force_tile
+VDA_KNOB(int, g_persist, -1);     // vda_debug_gemm_sched; -1 = automatic
+VDA_KNOB(int, g_stagger, -1);
+VDA_KNOB(int, g_desync, 0);       // vda_debug_gemm_desync
+// vda_debug_gemm_epi: the residual + row-statistics GEMMs (proj / fc2) through the register epilogue
+// (EK 2).  Off: bit-identical but measured slower than the staged epilogue (proj 94.8 -> 102.9 us,
+// fc2 320 -> 334 us at 43840 rows, same box, tools/ab_gemm.py).
+VDA_KNOB(int, g_res_epi, 0);
 
-// EK as gemm256_tile (1: bias, no residual / statistics; 2: bias + one residual + statistics).
-template <int ACT, bool LNF, int EK>
-__device__ __forceinline__ void gemm2_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem, bool pre,
-                                           int vb_next) {
-  using namespace g2;
-  static_assert(EK == 1 || EK == 2, "fixed epilogue kinds only");
-  static_assert(EK != 2 || (ACT == VDA_ACT_NONE && !LNF), "EK 2: no activation, no LN fold");
-  constexpr bool TAB = ACT == VDA_ACT_GELU;
-  const unsigned phib = phi_base(reinterpret_cast<const float*>(smem + NS * STG));
-  int tid;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave & 1, wn = wave >> 1;
-  int tile_m, tile_n;
-  tile_coords(vb, tiles_m * tiles_n, tiles_m, tiles_n, tile_m, tile_n);
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
-  const int nk = p.K / BKS;
-
-  // DMA: the stage is a stacked [X 128 rows; W 256 rows] x 64-B image, 24 pieces of 16 rows (1 KiB);
-  // wave w moves pieces w, w + 4, ..., w + 20 (pieces 0-7 are X, 8-23 W).  Lane: row piece*16 +
-  // lane/4, physical chunk lane & 3, logical chunk chunk_swz(row, lane & 3) (the same for every piece).
-  const int kc = chunk_swz(lane >> 2, lane & 3) * 8;
-  const __amdgpu_buffer_rsrc_t xrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)(unsigned)((long)p.M * p.ldx * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)(unsigned)((long)p.N * p.K * 2), 0x00020000);
-  auto offsets = [&](int m0_, int n0_, unsigned (&vo)[6]) {
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int R = (wave + 4 * i) * 16 + (lane >> 2);
-      if (i < 2) {
-        const int m = m0_ + R;
-        vo[i] = m < p.M ? (unsigned)(((long)m * p.ldx + kc) * 2) : 0x80000000u;
-      } else {
-        const int n = n0_ + R - BM;
-        vo[i] = n < p.N ? (unsigned)(((long)n * p.K + kc) * 2) : 0x80000000u;
-      }
-    }
-  };
-  auto stage = [&](int s, const unsigned (&vo)[6]) {
-    h16* base = smem + (s % NS) * STG;
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(i < 2 ? xrs : wrs, (VDA_LDS void*)(base + (wave + 4 * i) * 512), 16,
-                                               (int)vo[i], s * BKS * 2, 0, 0);
-  };
-  unsigned vo[6];
-  offsets(m0, n0, vo);
-  if (!pre) {
-    if constexpr (TAB) {  // once per block: the Phi table (8 KiB, two pieces per wave)
-      const char* src = reinterpret_cast<const char*>(g_phi_tab1k) + tid * 16;
-      glds16(src, smem + NS * STG + wave * 512);
-      glds16(src + 4096, smem + NS * STG + 2048 + wave * 512);
-    }
-    stage(0, vo);
-    stage(1, vo);
-    stage(2, vo);
-  }
-
-  f4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-
-  // fragment bases: W rows 128 + wn*128 + i*16 + frow, X rows wm*64 + j*16 + frow; the swizzle term
-  // depends on frow only, so fragment i / j sits a constant 512 halfs further
-  const int frow = lane & 15, fch = chunk_swz(frow, lane >> 4);
-  const int wbase = (BM + wn * 128 + frow) * BKS + fch * 8;
-  const int xbase = (wm * 64 + frow) * BKS + fch * 8;
-  // Two phases per K step s (16 MFMAs each), fragment reads always one phase ahead of their use:
-  //   A: read W4-7(s)                                  | MFMA W0-3 x X(s)
-  //   B: wait stage s+1, lgkmcnt(0), barrier; DMA stage | MFMA W4-7 x X(s)
-  //      s+3 into stage s's buffer (every wave's reads of it have landed); read W0-3(s+1), X(s+1)
-  // Three buffers hold stages s .. s+2; stage s+1 is waited for two steps after its issue.  The
-  // newer ops at a stage wait: the next stage (6 per wave) and, on a chained tile's first waits, the
-  // previous tile's NIT output stores issued after this tile's stages 0-2.
-  h8 wf[8], xa[4], xb[4];
-  auto rd_w = [&](int st_, int i0) {
-    const h16* sb = smem + (st_ % NS) * STG + wbase;
-#pragma unroll
-    for (int i = i0; i < i0 + 4; ++i) wf[i] = *reinterpret_cast<const h8*>(sb + i * 512);
-  };
-  auto rd_x = [&](int st_, h8 (&xf)[4]) {
-    const h16* sb = smem + (st_ % NS) * STG + xbase;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) xf[j] = *reinterpret_cast<const h8*>(sb + j * 512);
-  };
-  auto mma = [&](int i0, const h8 (&xf)[4]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = i0; i < i0 + 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(wf[i], xf[j], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  auto wait_stage = [&](bool newer_stage, bool stores) {
-    if (newer_stage) {
-      if (stores) wait_vmcnt<6 + NIT>(); else wait_vmcnt<6>();
-    } else {
-      if (stores) wait_vmcnt<NIT>(); else wait_vmcnt<0>();
-    }
-  };
-  // stage 0 (stages 1, 2 and the chained stores may stay in flight)
-  if (pre) wait_vmcnt<12 + NIT>(); else wait_vmcnt<12>();
-  __builtin_amdgcn_s_barrier();
-  rd_w(0, 0);
-  rd_x(0, xa);
-  auto step = [&](int s_, h8 (&xc)[4], h8 (&xn)[4]) {
-    rd_w(s_, 4);
-    mma(0, xc);
-    const bool more = s_ + 1 < nk;
-    if (more) wait_stage(s_ + 2 < nk, pre && s_ < 2);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): W4-7(s) landed, stage s's buffer is free
-    __builtin_amdgcn_s_barrier();
-    if (s_ + 3 < nk) stage(s_ + 3, vo);
-    if (more) {
-      rd_w(s_ + 1, 0);
-      rd_x(s_ + 1, xn);
-    }
-    mma(4, xc);
-  };
-  for (int s = 0; s < nk; s += 2) {  // unrolled by two: X fragments alternate between xa and xb
-    step(s, xa, xb);
-    if (s + 1 < nk) step(s + 1, xb, xa);
-  }
-
-  // ---- epilogue ----
-  const vda_epilogue& e = p.epi;
-  const int mcol = lane & 15, nq = (lane >> 4) * 4;
-  // per-channel operands and the rows' LN statistics, from L2 (the other block covers the latency)
-  f4 bv[8], cv[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int n = n0 + wn * 128 + i * 16 + nq;
-    const int nc = n < p.N ? n : 0;
-    bv[i] = *reinterpret_cast<const f4*>(e.bias + nc);
-    if constexpr (LNF) cv[i] = *reinterpret_cast<const f4*>(e.ln_colsum + nc);
-  }
-  float2 mr[4];
-  if constexpr (LNF) {
-    const int P = e.ln_parts;
-    const float invK = 1.f / (float)p.K;
-    int mc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int m = m0 + wm * 64 + j * 16 + mcol;
-      mc[j] = m < p.M ? m : 0;
-    }
-    if (P <= 0) {  // (mean, rstd) per row (vda_row_stats)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mr[j] = *reinterpret_cast<const float2*>(e.ln_stats + 2L * mc[j]);
-    } else {  // P <= 4 partial (sum, sumsq): all loads issued (clamped) before any is used
-      float2 pq[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-          pq[j][t] = *reinterpret_cast<const float2*>(e.ln_stats + 2L * ((long)mc[j] * P + (t < P ? t : 0)));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        float sm = 0.f, sq = 0.f;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          sm += t < P ? pq[j][t].x : 0.f;
-          sq += t < P ? pq[j][t].y : 0.f;
-        }
-        const float mean = sm * invK;
-        mr[j] = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq * invK), 0.f) + e.ln_eps));
-      }
-    }
-  }
-  // residual rows of phase 2, requested now so they land under the activation / staging work
-  const int q = tid & 31, row0 = tid >> 5;  // phase 2: row0 + 8 it, 16-B chunk q
-  const int c = n0 + q * 8;
-  const long mrows = p.M - m0;
-  auto rsrc = [&](const h16* base, long ld) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (long)m0 * ld), (short)0,
-                                             (int)(mrows * ld * 2 < 0x7fffffffL ? mrows * ld * 2 : 0x7fffffffL), 0x00020000);
-  };
-  auto voff = [&](long ld) { return c < p.N ? (unsigned)(((long)row0 * ld + c) * 2) : 0x80000000u; };
-  h8 rpre[EK == 2 ? NIT : 1];
-  if constexpr (EK == 2) {
-    const __amdgpu_buffer_rsrc_t rr = rsrc((const h16*)e.res, e.ldres);
-    const unsigned vr = voff(e.ldres), sr = (unsigned)(8 * e.ldres * 2);
-#pragma unroll
-    for (int it = 0; it < NIT; ++it)
-      rpre[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, vr + it * sr, 0, 0));
-  }
-  // every wave is done reading the operand stages before the output tile is staged over them
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f4 v = acc[i][j];
-      if constexpr (LNF) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = fmaf(mr[j].y, fmaf(-mr[j].x, cv[i][r], v[r]), bv[i][r]);
-      } else {
-        v += bv[i];
-      }
-      if constexpr (TAB) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = gelu_tab1k(v[r], phib);
-      }
-      typedef float f2v __attribute__((ext_vector_type(2)));
-      const h2 lo = __builtin_convertvector(f2v{v[0], v[1]}, h2);
-      const h2 hi = __builtin_convertvector(f2v{v[2], v[3]}, h2);
-      const int ml = wm * 64 + j * 16 + mcol;
-      const int u = ((wn * 128 + i * 16 + nq) >> 2) ^ (ml & 15);
-      *reinterpret_cast<uint2*>(&smem[ml * BN + u * 4]) = make_uint2(__builtin_bit_cast(unsigned, lo), __builtin_bit_cast(unsigned, hi));
-    }
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_s_barrier();
-  // phase 2: the staged tile back into registers (rows row0 + 8 it alternate the swizzle's bit 3)
-  h8 tv[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int row = row0 + 8 * it, sw = row & 15;
-    const uint2 lo = *reinterpret_cast<const uint2*>(smem + row * BN + ((2 * q) ^ sw) * 4);
-    const uint2 hi = *reinterpret_cast<const uint2*>(smem + row * BN + ((2 * q + 1) ^ sw) * 4);
-    tv[it] = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
-  }
-  if (vb_next >= 0) {  // chain: the next tile's stages 0-2 into the freed buffers, before the stores
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    int tmn, tnn;
-    tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
-    unsigned von[6];
-    offsets(tmn * BM, tnn * BN, von);
-    stage(0, von);
-    stage(1, von);
-    stage(2, von);
-  }
-  const __amdgpu_buffer_rsrc_t ry = rsrc(p.y, p.ldy);
-  const unsigned vy = voff(p.ldy), sy = (unsigned)(8 * p.ldy * 2);
-  if constexpr (EK == 2) {  // + residual, + per-row partial (sum, sumsq) of the stored values
-    const bool cval = c < p.N;
-    float v[32];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const h8 t = tv[it] + rpre[it];
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
-      stat_acc(cval ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, v[it], v[16 + it]);
-    }
-    const float r = halfwave_sum32(v, lane);
-    const int P = (p.N + 255) / 256;
-    const int m = m0 + row0 + 8 * (lane & 15);
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)e.stats_out, (short)0, (int)((long)p.M * P * 8), 0x00020000);
-    const unsigned vo2 = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + ((lane >> 4) & 1)) * 4) : 0x80000000u;
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, vo2, 0, 0);
-  } else {
-#pragma unroll
-    for (int it = 0; it < NIT; ++it)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tv[it]), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
-  }
-}
-
-// Persistent: 2 blocks per CU walk tiles vb, vb + gridDim.x, ...; blocks of the second half start
-// start_ticks (100 MHz) late so the two blocks of a CU begin out of phase.
-template <int ACT, bool LNF, int EK>
-__global__ __launch_bounds__(256, 2) void gemm2_kernel(GemmParams p, int tiles_m, int tiles_n, int start_ticks) {
-  constexpr bool TAB = ACT == VDA_ACT_GELU;
-  __shared__ __attribute__((aligned(1024))) h16 smem[g2::NS * g2::STG + (TAB ? g2::PHI_HALVES : 0)];
-  const int ntiles = tiles_m * tiles_n;
-  if (start_ticks > 0 && 2 * (int)blockIdx.x >= (int)gridDim.x) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)start_ticks) __builtin_amdgcn_s_sleep(8);
-  }
-  bool pre = false;
-  for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
-    const int nxt = vb + (int)gridDim.x;
-    gemm2_tile<ACT, LNF, EK>(p, vb, tiles_m, tiles_n, smem, pre, nxt < ntiles ? nxt : -1);
-    pre = true;
-  }
-}
-
-int g_force_tile = -1;  // debug / tuning override (vda_debug_force_tile)
-int g_persist = -1, g_stagger = -1;  // debug overrides (vda_debug_gemm_sched); -1 = automatic
-int g_desync = 0;                     // tuning experiment (vda_debug_gemm_desync)
-
-int cu_count() {
-  static int cached[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (dev < 0 || dev >= 64) return 256;
-  if (!cached[dev]) {
-    int n = 0;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-    cached[dev] = n;
-  }
-  return cached[dev];
-}
+int cu_count() { return vda_cu_count(); }
 
 // grid and start stagger of a phased launch (see gemm256_kernel)
 void phased_sched(int ntiles, int nk, bool conv, int& grid, int& ticks) {
@@ -1901,32 +1584,6 @@ void launch_tile(const GemmParams& p, hipStream_t st) {
                      0, st, p, tiles_m, tiles_n);
 }
 
-int g_gemm2 = -1;        // two-blocks-per-CU kernel: -1 automatic, 0 never, 1 every shape it serves (A/B)
-int g_gemm2_ticks = 0;   // start offset of the second half of its blocks (100 MHz ticks)
-
-// gemm2_kernel for the fixed epilogue kinds (dense, activation none / GELU); false = not served
-template <int ACT>
-bool launch_gemm2(const GemmParams& p, int ek, hipStream_t st) {
-  if (g_gemm2 <= 0 || (ACT != VDA_ACT_NONE && ACT != VDA_ACT_GELU) || p.K % 32 != 0 || p.K < 96) return false;
-  const int tiles_m = (p.M + g2::BM - 1) / g2::BM, tiles_n = (p.N + g2::BN - 1) / g2::BN;
-  const int grid = std::min(tiles_m * tiles_n, (g_gemm2 == 2 ? 1 : 2) * cu_count());
-  const bool lnf = p.epi.ln_stats != nullptr;
-  if (ek == 1) {
-    if (lnf)
-      hipLaunchKernelGGL((gemm2_kernel<ACT, true, 1>), dim3(grid), dim3(256), 0, st, p, tiles_m, tiles_n, g_gemm2_ticks);
-    else
-      hipLaunchKernelGGL((gemm2_kernel<ACT, false, 1>), dim3(grid), dim3(256), 0, st, p, tiles_m, tiles_n, g_gemm2_ticks);
-    return true;
-  }
-  if constexpr (ACT == VDA_ACT_NONE) {
-    if (ek == 2 && !lnf) {
-      hipLaunchKernelGGL((gemm2_kernel<ACT, false, 2>), dim3(grid), dim3(256), 0, st, p, tiles_m, tiles_n, g_gemm2_ticks);
-      return true;
-    }
-  }
-  return false;
-}
-
 template <int XR, int WR, bool CONV, int ACT>
 void launch_phased(const GemmParams& p, hipStream_t st) {
   const int BM = 128 * XR, BN = 128 * WR;
@@ -1943,10 +1600,6 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
   if constexpr (!CONV && XR == 2 && (ACT == VDA_ACT_NONE || ACT == VDA_ACT_GELU)) {
     const vda_epilogue& e = p.epi;
     const bool rows1 = e.store == VDA_STORE_ROWS && e.bias && !e.gamma && !e.res2 && !e.rowbias;
-    if (g_gemm2 >= 1 && rows1) {
-      const int ek = (!e.res && !e.stats_out) ? 1 : (e.res && e.stats_out && !e.ln_stats) ? 2 : 0;
-      if (ek && launch_gemm2<ACT>(p, ek, st)) return;
-    }
     if (e.ln_stats) {
       if (rows1 && !e.res && !e.stats_out)
         hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false, true, 1>), dim3(grid), dim3(512), 0, st, p, tiles_m,
@@ -1962,7 +1615,7 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
       return;
     }
     if constexpr (ACT == VDA_ACT_NONE) {
-      if (rows1 && e.res && e.stats_out) {
+      if (g_res_epi && rows1 && e.res && e.stats_out) {
         hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false, false, 2>), dim3(grid), dim3(512), 0, st, p, tiles_m,
                            tiles_n, ticks, g_desync);
         return;
@@ -2264,6 +1917,7 @@ extern "C" int64_t vda_depth_head_workspace(int32_t BT, int32_t Hin, int32_t Win
   return (int64_t)BT * Ho * Wo * C * 2;
 }
 
+#ifdef VDA_TUNING
 extern "C" int vda_debug_force_tile(int32_t cfg) {
   g_force_tile = cfg;
   return 0;
@@ -2274,21 +1928,14 @@ extern "C" int vda_debug_gemm_desync(int32_t groups) {
   return 0;
 }
 
-extern "C" int vda_debug_gemm2(int32_t mode, int32_t start_ticks) {
-  g_gemm2 = mode;
-  g_gemm2_ticks = start_ticks;
-  if (mode == 99) {  // report the resident blocks per CU of the fc1 / fc2 instantiations
-    int a = 0, b = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, (const void*)gemm2_kernel<VDA_ACT_GELU, true, 1>, 256, 0);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, (const void*)gemm2_kernel<VDA_ACT_NONE, false, 2>, 256, 0);
-    g_gemm2 = -1;
-    return a * 10 + b;
-  }
-  return 0;
-}
-
 extern "C" int vda_debug_gemm_sched(int32_t persist_blocks, int32_t stagger) {
   g_persist = persist_blocks;
   g_stagger = stagger;
   return 0;
 }
+
+extern "C" int vda_debug_gemm_epi(int32_t res_register) {
+  g_res_epi = res_register;
+  return 0;
+}
+#endif

@@ -328,7 +328,8 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
 
 }  // namespace
 
-int g_hconv_mode = -1;  // vda_debug_hconv: -1 automatic, 0 never, 1 every served shape
+// vda_debug_hconv (tuning build): -1 automatic, 0 never, 1 every served shape
+VDA_KNOB(int, g_hconv_mode, -1);
 
 // Does the halo kernel serve (and, in automatic mode, win on) this conv?
 bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout) {
@@ -359,7 +360,9 @@ int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int
   return 0;
 }
 
+#ifdef VDA_TUNING
 extern "C" int vda_debug_hconv(int32_t mode) {
   g_hconv_mode = mode;
   return 0;
 }
+#endif

@@ -13,6 +13,18 @@ int vda_set_error(int code, const char* msg) {
   return code;
 }
 
+int vda_cu_count() {
+  static int cus[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cus[dev] == 0) {  // benign race: every thread stores the same device property
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    cus[dev] = n;
+  }
+  return cus[dev];
+}
+
 extern "C" const char* vda_version(void) { return "libvda 0.2 (gfx950, fp16 MFMA)"; }
 extern "C" int64_t vda_epilogue_size(void) { return (int64_t)sizeof(vda_epilogue); }
 extern "C" const char* vda_last_error(void) { return g_err; }

@@ -243,18 +243,9 @@ __global__ __launch_bounds__(256) void strip_finish_kernel(const float* __restri
   }
 }
 
-int g_st_cus = 0;
-int g_st_force_split = 0;  // tuning override (vda_debug_strip_split)
+VDA_KNOB(int, g_st_force_split, 0);  // vda_debug_strip_split (tuning build); 0 = automatic
 
-int st_cus() {
-  if (g_st_cus == 0) {
-    int dev = 0, n = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    g_st_cus = n > 0 ? n : 256;
-  }
-  return g_st_cus;
-}
+int st_cus() { return vda_cu_count(); }
 
 // Split count for a served shape: minimise rounds x steps-per-item, charging a split its workspace
 // round trip (s slices written + read, ~4 TB/s) in units of a ~1.1 us pipeline step.  Only splits whose
@@ -280,10 +271,12 @@ int st_split(int BT, int H, int W, int Cin, long ws_floats) {
 
 }  // namespace
 
+#ifdef VDA_TUNING
 extern "C" int vda_debug_strip_split(int32_t nsplit) {
   g_st_force_split = nsplit;
   return 0;
 }
+#endif
 
 bool vda_conv_strip_serves(int W, int Cin, int Cout) {
   return Cout == ST_N && Cin % ST_SLAB == 0 && W <= ST_MAXW && W >= 16;
