@@ -15,20 +15,25 @@ from collections import defaultdict
 # as kernels evolve; bench.py looks its figures up by tag).  Template arguments of gemm256_kernel:
 # <XR, WR, CONV, ACT, ROWB, LNF, EK>; ACT 1 = GELU; LNF = LayerNorm folded into the epilogue.
 TAGS = [
-    (r"^gemm256_kernel<2, 2, false, 1, false, true\b", "enc_fc1"),        # norm2 + fc1 + GELU
-    (r"^gemm256_kernel<2, 2, false, 0, false, true\b", "enc_qkv"),        # norm1 + qkv
-    (r"^gemm256_kernel<2, 2, false, 0, false, false\b", "enc_proj_fc2"),  # proj / fc2 + residual + row stats
+    (r"^gemm256_kernel<2, 2, false, 1, false, true\b", "enc_fc1"),            # norm2 + fc1 + GELU (register epilogue)
+    (r"^gemm256_kernel<2, 2, false, 0, false, true\b", "enc_qkv"),            # norm1 + qkv (register epilogue)
+    (r"^gemm256_kernel<2, 2, false, 0, false, false, 0>", "gemm_staged"),      # proj / fc2 (+ residual, row stats) and others
+    (r"^gemm256_kernel<2, 2, false, 0, false, false, 1>", "gemm_bias_rows"),
+    (r"^gemm256_kernel<2, 2, false, 0, true\b", "gemm_rowbias"),
+    (r"^gemm256_kernel<2, 2, false, 2\b", "gemm_geglu"),
     (r"^gemm256_kernel<2, 2, true\b", "conv_phased"),
-    (r"^spatial_attn32_kernel", "spatial_attention"),
-    (r"^temporal_attn_lds_kernel", "temporal_attention"),
-    (r"^depth_conv_kernel", "depth_conv"),
-    (r"^halo_conv_kernel<64, 128, 1", "output_conv1"),
-    (r"^hconv_kernel|^halo256", "conv3x3_halo256"),
+    (r"spatial_attn32_kernel", "spatial_attention"),
+    (r"temporal_attn_lds_kernel", "temporal_attention"),
+    (r"depth_conv_kernel", "depth_conv"),
+    (r"halo_conv_kernel<64, 128, 1|halo_conv_kernelILi64ELi128ELi1E", "output_conv1"),
+    (r"^hconv256_kernel", "conv3x3_halo256"),
     (r"^strip_conv", "conv3x3_strip"),
 ]
 
 
 def tag_of(name):
+    name = re.sub(r"^void ", "", name)
+    name = re.sub(r"^_ZN12_GLOBAL__N_1\d+", "", name)  # mangled anonymous-namespace kernels
     for rx, t in TAGS:
         if re.search(rx, name):
             return t

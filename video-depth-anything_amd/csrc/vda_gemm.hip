@@ -28,6 +28,9 @@ extern "C" int vda_debug_timestamps(void* host) {
 #define TS(k) do {} while (0)
 #endif
 #include "../../include/vda.h"
+#ifndef VDA_GEXP  // main-loop timing experiments (tools/build_variants.sh; 0 = the kernel)
+#define VDA_GEXP 0
+#endif
 
 // cache policy of the phased epilogue's output stores: nt (aux = 2).  In-situ A/B on one box
 // (tools/ab_libs.sh, 2 rounds): every phased GEMM/conv class 0.7-3.6 % faster, the forward's kernel
@@ -952,7 +955,9 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         wf[i][ks] = *reinterpret_cast<const h8*>(&base[woff + swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
   };
   auto mma = [&](int qm, int qn) {
+#if VDA_GEXP < 4
     __builtin_amdgcn_s_barrier();
+#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -965,7 +970,9 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           acc[qn * 2 + i][qm * 4 + j] = mfma16(wf[i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+#if VDA_GEXP < 3
     __builtin_amdgcn_s_barrier();
+#endif
   };
 
   // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
@@ -975,27 +982,38 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     const int cb = kt & 1, nb = cb ^ 1;
     const h16* base = smem + cb * BUF;
     const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
+#if VDA_GEXP >= 2  // timing experiments only (results wrong): no operand DMA in the loop
+    (void)more1; (void)more2; (void)nb;
+#define VDA_STAGE(...) do {} while (0)
+#else
+#define VDA_STAGE(...) __VA_ARGS__
+#endif
     // P1
     load_x(base, 0);
     load_w(base, 0);
-    if (more1) stage_x(kt + 1, nb, 1);
+    if (more1) VDA_STAGE(stage_x(kt + 1, nb, 1));
     mma(0, 0);
     // P2
     load_w(base, 1);
-    if (more1) stage_w(kt + 1, nb, 0);
+    if (more1) VDA_STAGE(stage_w(kt + 1, nb, 0));
     mma(0, 1);
     // P3
     load_x(base, 1);
-    if (more2) stage_x(kt + 2, cb, 0);
+    if (more2) VDA_STAGE(stage_x(kt + 2, cb, 0));
     mma(1, 1);
     // P4: retire everything but this tile's two P3/P4 quarters
     load_w(base, 0);
+#if VDA_GEXP == 0
     if (more2) {
       stage_w(kt + 2, cb, 1);
       wait_vmcnt<XR + WR>();
     } else {
       wait_vmcnt<0>();
     }
+#elif VDA_GEXP == 1
+    if (more2) stage_w(kt + 2, cb, 1);
+#endif
+#undef VDA_STAGE
     mma(1, 0);
   }
   if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
