@@ -209,8 +209,9 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 // per gap for the softmax VALU, the 16x16x32 one only 8).  Block = 4 waves x 32 queries of one
 // (batch, head); a wave owns 32 query columns, a lane q = lane & 31 and half hf = lane >> 5.
 //   Sᵀ[key][q] = K·Qᵀ   A = K rows (LDS, ds_read_b128), B = Q (registers, pre-scaled by scale·log2e);
-//                       the chain starts from C = -m (a 16-register tile of the running max), so
-//                       the scores come out relative to the max with no VALU subtraction.
+//                       the chain starts from C = -m (a 16-register tile of the running reference
+//                       m, see the deferred re-base below), so the scores come out relative to it
+//                       with no VALU subtraction.
 //   Oᵀ += Vᵀ·Pᵀ         B = P straight from the Sᵀ registers (k order 16st + 8(j>>2) + 4hf + (j&3)),
 //                       A = Vᵀ by ds_read_b64_tr_b16 in the same permuted key order.
 // K/V tiles (64 keys x 64 channels, 8 KiB each) arrive by LDS-DMA into a 3-deep ring (4 x 1-KiB
@@ -218,6 +219,9 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 // query block) map keeps all query blocks of one (b, h) on one XCD (K/V re-reads hit that L2).
 // LDS images: K slot row*8 + (chunk ^ ((row >> 1) & 7)), V slot row*8 + (chunk ^ (((row >> 1) & 1) << 2)):
 // conflict-free for the b128 K reads and the b64 transposed V reads (brute-forced).
+// 152 VGPRs: three blocks per CU (3 x 48 KiB of LDS).  Measured and rejected (tools/ab_attn.py):
+// issuing the QK MFMAs of tile t+1 before the softmax of tile t (213 VGPRs, a 4-slot ring, two blocks
+// per CU) 333 vs 292 us; with the per-tile max still computed, 354 vs 320 us.
 // =============================================================================================
 constexpr int SA_KT = 64;    // keys per tile
 constexpr int SA_QB = 128;   // queries per block
@@ -278,68 +282,107 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
   float mrun = 0.f, lsum = 0.f;
   const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
 
+  // Lane-constant LDS byte offsets: K fragment ks of key row r32 (key block kb adds 32 rows = 4 KiB),
+  // transposed-V read base of output tile dt (key slice ps adds 16 rows = 2 KiB, the second read of
+  // a fragment 8 rows = 1 KiB).  The swizzle terms depend on the lane only, so per tile the reads
+  // cost one address add per ks / dt and the rest are immediate offsets.
+  unsigned kofs[4], vofs[2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) kofs[ks] = (unsigned)sa_kslot(r32, ks * 2 + hf) * 16u;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    const int col = dt * 32 + (grp & 1) * 16 + 4 * p4, r0 = 4 * (grp >> 1) + q4;
+    vofs[dt] = (unsigned)(sa_vslot(r0, col >> 3) * 8 + (col & 7)) * 2u;
+  }
+  // Deferred re-base (FA-style online softmax without a per-tile max): P = exp2(S - m) against the
+  // running reference m; a tile only re-bases when a lane's P sum passes 2^15 (then some P may not
+  // fit fp16: the scores are recomputed, the true tile max taken and the tile redone), so the steady
+  // state computes no max at all.  P <= 2^15 keeps P exact to fp16 rounding and the fp32 sums far
+  // from overflow.
   auto tile = [&](int kt, auto first_tag, auto mask_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MASK = decltype(mask_tag)::value;
-    const h16* sk = sKV[kt % SA_NBUF][0];
-    const h16* sv = sKV[kt % SA_NBUF][1];
-    f16x s[2];
+    // ring slot byte offset through an opaque scalar move: the compiler would otherwise strength-reduce
+    // kt % 3 into per-read address updates (two VALU per read)
+    unsigned bo;
+    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % SA_NBUF), "n"(2 * SA_KT * SD * 2));
+    const char* kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
+    const char* vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
+    f16x sc[2];
+    auto qk = [&]() {
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
+      for (int ks = 0; ks < 4; ++ks) {  // the two key blocks' accumulation chains interleaved
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const h8 kf = *reinterpret_cast<const h8*>(&sk[sa_kslot(kb * 32 + r32, ks * 2 + hf) * 8]);
-        s[kb] = mfma32(kf, qf[ks], ks == 0 ? negm : s[kb]);
+        for (int kb = 0; kb < 2; ++kb) {
+          const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
+          sc[kb] = mfma32(kf, qf[ks], ks == 0 ? negm : sc[kb]);
+        }
       }
-    }
-    if constexpr (MASK) {
+      if constexpr (MASK) {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) sc[kb][r] = -INFINITY;
+      }
+    };
+    qk();
+    auto tile_max = [&]() {
+      float mx = fmaxf(fmaxf(sc[0][0], sc[0][1]), sc[0][2]);
+#pragma unroll
+      for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[0][r]), sc[0][r + 1]);
+      mx = fmaxf(fmaxf(mx, sc[0][15]), sc[1][0]);
+#pragma unroll
+      for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[1][r]), sc[1][r + 1]);
+      mx = fmaxf(mx, sc[1][15]);
+      return half_max(mx);
+    };
+    auto rebase = [&](float sh) {
+      mrun += sh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) negm[r] = -mrun;
+      sc[0] -= sh;
+      sc[1] -= sh;
+    };
+    h8 pf[4];
+    float t0, t1;
+    auto expo = [&]() {
+      t0 = 0.f;
+      t1 = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) s[kb][r] = -INFINITY;
-    }
-    float mx = fmaxf(fmaxf(s[0][0], s[0][1]), s[0][2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[0][r]), s[0][r + 1]);
-    mx = fmaxf(fmaxf(mx, s[0][15]), s[1][0]);
-#pragma unroll
-    for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s[1][r]), s[1][r + 1]);
-    mx = fmaxf(mx, s[1][15]);
-    mx = half_max(mx);
-    // deferred rescale: keep a stale max while the tile max exceeds it by <= 8 (P <= 2^8: exact in
-    // fp16 P and fp32 sums); the first tile always re-bases
-    if (FIRST || __any(mx > 8.f)) {
-      const float sh = FIRST ? mx : fmaxf(mx, 0.f);
-      mrun += sh;
-      if (!FIRST) {
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
+          if (kb == 0) t0 += pv;
+          else t1 += pv;
+          pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
+        }
+    };
+    if constexpr (FIRST) {
+      rebase(tile_max());
+      expo();
+    } else {
+      expo();
+      if (__any(!(t0 + t1 <= 32768.f))) {  // rare: re-base on the true tile max and redo the tile
+        qk();  // the scores again (the K slot is still resident): they need not stay live past expo
+        const float sh = fmaxf(tile_max(), 0.f);
         const float alpha = __builtin_amdgcn_exp2f(-sh);
         lsum *= alpha;
         o[0] *= alpha;
         o[1] *= alpha;
+        rebase(sh);
+        expo();
       }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) negm[r] = -mrun;
-      s[0] -= sh;
-      s[1] -= sh;
     }
-    h8 pf[4];
+    lsum += t0 + t1;
 #pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
+    for (int ps = 0; ps < 4; ++ps) {  // the two output tiles' chains interleaved
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(s[kb][r]);
-        lsum += p;
-        pf[kb * 2 + (r >> 3)][r & 7] = (h16)p;
-      }
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        const int col = dt * 32 + (grp & 1) * 16 + 4 * p4;
-        const int r0 = ps * 16 + 4 * (grp >> 1) + q4;
-        const h4 v0 = lds_read_tr16(&sv[sa_vslot(r0, col >> 3) * 8 + (col & 7)]);
-        const h4 v1 = lds_read_tr16(&sv[sa_vslot(r0 + 8, col >> 3) * 8 + (col & 7)]);
+      for (int dt = 0; dt < 2; ++dt) {
+        const char* va = vbase + vofs[dt] + ps * 2048;
+        const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
+        const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
         const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
         o[dt] = mfma32(vf, pf[ps], o[dt]);
       }

@@ -28,6 +28,12 @@ extern "C" int vda_debug_timestamps(void* host) {
 #define TS(k) do {} while (0)
 #endif
 #include "../../include/vda.h"
+#ifndef VDA_PH2  // phased GEMM main loop: 2 phases per K tile (32 MFMAs between barriers) instead of 4
+#define VDA_PH2 0
+#endif
+#ifndef VDA_EEXP  // register-epilogue timing experiments (1: no GELU, 2: no stores; results wrong)
+#define VDA_EEXP 0
+#endif
 #ifndef VDA_GEXP  // main-loop timing experiments (tools/build_variants.sh; 0 = the kernel)
 #define VDA_GEXP 0
 #endif
@@ -688,7 +694,7 @@ constexpr int phased_nit() {
 // whose vmcnt(0) would drain the chained stores at every tile start).
 template <int XR, int WR, bool CONV, int ACT, bool ROWB, bool LNF, int EK>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
 __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem,
-                                             bool pre, int vb_next) {
+                                             bool pre, int vb_next, int wave_in) {
   // ROWB: per-row bias support (a separate instantiation: its row-index division would otherwise
   // raise the register pressure of every phased GEMM past the spill point)
   // LNF: LayerNorm folded into the GEMM (vda_epilogue.ln_stats / ln_colsum): X is the raw residual
@@ -714,12 +720,14 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   const unsigned phib = phi_base(phi_lds);
   h16* lnst_lds = smem + 2 * BUF + (TAB ? PHI_LDS_HALVES : 0);  // LNF: [256][2] fp32 (mean, rstd)
 
-  // thread id laundered through a volatile move: every lane-derived address below is recomputed
-  // per tile instead of being hoisted out of the persistent tile loop (and spilled across it)
-  int tid;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // lane id rebuilt per tile by a volatile mbcnt (and the wave index passed in an SGPR): every
+  // lane-derived address below is recomputed per tile instead of being hoisted out of the persistent
+  // tile loop, and threadIdx (v0) need not stay live across it (its spill reload's vmcnt(0) at the
+  // loop head would drain the chained prologue DMA and stores)
+  int lane, wave;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  asm volatile("s_mov_b32 %0, %1" : "=s"(wave) : "s"(wave_in));
+  const int tid = wave * 64 + lane;
   const int wm = wave % XR, wn = wave / XR;
   int tile_m, tile_n;
   tile_coords(vb, tiles_m * tiles_n, tiles_m, tiles_n, tile_m, tile_n);
@@ -863,6 +871,15 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
+  constexpr bool PH2 = VDA_PH2 != 0 && EK == 1;
+  // the next tile's prologue, issued by a chaining epilogue: K tile 0 (and the two K-tile-1 quarters
+  // the 4-phase loop expects from "tile -1")
+  auto chain_dma = [&](const unsigned (&xn)[XR][2], const unsigned (&wn2)[WR][2]) {
+    bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
+    if constexpr (!PH2) {
+      if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+    }
+  };
   const int frow = lane & 15, fchunk = lane >> 4;
   const bool prerelu = CONV && p.pre_relu;
   // wave's regions: X half wm (rows 0..127 of it), W half wn>>1 at row offset (wn&1)*64
@@ -896,7 +913,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     lnst_dma(m0);
     TS(1);
     stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
-    if (nk > 1) {
+    if (!PH2 && nk > 1) {
       stage_x(1, 1, 0); stage_w(1, 1, 1);
       wait_vmcnt<XR + WR>();
     } else {
@@ -904,7 +921,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     }
   } else {
     // issued by the previous tile's epilogue, followed by at least NIT_EPI output stores
-    if (nk > 1) wait_vmcnt<XR + WR + NIT_EPI>();
+    if (!PH2 && nk > 1) wait_vmcnt<XR + WR + NIT_EPI>();
     else wait_vmcnt<NIT_EPI>();
   }
   __builtin_amdgcn_s_barrier();
@@ -975,6 +992,63 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
 #endif
   };
 
+  if constexpr (PH2) {
+    // Two phases per K tile, 32 MFMAs each: A = X rows q0 x all 64 W columns, B = X rows q1 x the same
+    // W fragments (held in registers across both).  A barrier interval (one wave per SIMD in its MFMA
+    // segment, the other reading LDS / issuing DMA) then spans 512 MFMA cycles instead of 256, halving
+    // the barrier count per K tile.  DMA: K tile t+1 goes into the other buffer, W + X q0 in A(t),
+    // X q1 in B(t), each >= 2 intervals after that region's last read (lagging waves included) and
+    // retired two intervals after issue, before the barrier that precedes its first read.
+    h8 wg[2][2][2];
+    auto load_w2 = [&](const h16* base, int qn) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          wg[qn][i][ks] = *reinterpret_cast<const h8*>(&base[woff + swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
+    };
+    auto mma2 = [&](int qm) {
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[qn * 2 + i][qm * 4 + j] = mfma16(wg[qn][i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+    };
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cb = kt & 1, nb = cb ^ 1;
+      const h16* base = smem + cb * BUF;
+      const bool more1 = kt + 1 < nk;
+      // A: also retires X q1 of this tile (issued in B(t-1))
+      load_x(base, 0);
+      load_w2(base, 0);
+      load_w2(base, 1);
+      if (more1) {
+        stage_w(kt + 1, nb, 0); stage_w(kt + 1, nb, 1); stage_x(kt + 1, nb, 0);
+        wait_vmcnt<2 * WR + XR>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      mma2(0);
+      // B: retires W + X q0 of tile t+1
+      load_x(base, 1);
+      if (more1) {
+        stage_x(kt + 1, nb, 1);
+        wait_vmcnt<XR>();
+      }
+      mma2(1);
+    }
+  } else
   // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
   // and retired by the P4 wait one phase before its first read:
   //   P1: Xq1(t+1) -> other buffer   P2: Wq0(t+1) -> other   P3: Xq0(t+2) -> this   P4: Wq1(t+2) -> this
@@ -1060,8 +1134,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         unsigned xn[XR][2], wn2[WR][2];
         dense_offsets(tmn * BM, tnn * BN, xn, wn2);
         lnst_dma(tmn * BM);
-        bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
-        if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+        chain_dma(xn, wn2);
       }
     }
     static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
@@ -1089,10 +1162,10 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         } else {
           v[i] += pbv[i];
         }
-        if constexpr (ACT == VDA_ACT_GELU && TAB) {
+        if constexpr (ACT == VDA_ACT_GELU && TAB && VDA_EEXP != 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_tab(v[i][r], phib);
-        } else if constexpr (ACT == VDA_ACT_GELU) {
+        } else if constexpr (ACT == VDA_ACT_GELU && VDA_EEXP != 1) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_erf(v[i][r]);
         }
@@ -1111,7 +1184,12 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
         const u32x4 o = {__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
                          __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+#if VDA_EEXP == 2
+        asm volatile("" :: "v"(o));
+        (void)ry; (void)rofs;
+#else
         __builtin_amdgcn_raw_buffer_store_b128(o, ry, rofs + cofs[pp], 0, VDA_EPI_STORE_AUX);
+#endif
       }
     }
     TS(5);
@@ -1154,8 +1232,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
         unsigned xn[XR][2], wn2[WR][2];
         dense_offsets(tmn * BM, tnn * BN, xn, wn2);
-        bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
-        if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+        chain_dma(xn, wn2);
       }
     }
     static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
@@ -1416,8 +1493,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         unsigned xn[XR][2], wn2[WR][2];
         dense_offsets(tmn * BM, tnn * BN, xn, wn2);
         lnst_dma(tmn * BM);
-        bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
-        if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
+        chain_dma(xn, wn2);
       }
     }
     auto phase2 = [&](auto nres_tag) {
@@ -1535,6 +1611,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0) +
                                                      (EK == 2 ? 4096 : 0)];
   const int ntiles = tiles_m * tiles_n;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
     const uint64_t d = (uint64_t)(((blockIdx.x >> 3) % desync) * stagger_ticks / desync);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1546,16 +1623,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   if constexpr (CONV) {  // convs launch one block per tile (phased_sched): no loop-carried state
     const int vb = blockIdx.x;
     TS(0);
-    gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, false, -1);
+    gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, false, -1, wave);
     TS(7);
   } else {
     // row-store epilogues chain the next tile's prologue (gemm256_tile); the scatter store does not
-    const bool chain = EK ? true : p.epi.store == VDA_STORE_ROWS;
+#ifndef VDA_CHAIN_STAGED  // chain the staged row-store epilogue too: measured 4 % slower on proj (106.0
+#define VDA_CHAIN_STAGED 0  // -> 110.3 us, same box), fc2 unchanged; the register epilogues always chain
+#endif
+    const bool chain = EK ? true : (VDA_CHAIN_STAGED && p.epi.store == VDA_STORE_ROWS);
     bool pre = false;
     for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
       TS(0);
       const int nxt = vb + (int)gridDim.x;
-      gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, pre, chain && nxt < ntiles ? nxt : -1);
+      gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, pre, chain && nxt < ntiles ? nxt : -1, wave);
       if (!chain) __syncthreads();
       pre = chain;
       TS(7);
