@@ -211,6 +211,34 @@ def test_spatial_attention(B, N, H):
     assert rel(y, ref) < 3e-3
 
 
+@pytest.mark.parametrize("ramp", ["up", "spike", "down"])
+def test_spatial_attention_rebase(ramp):
+    """The online softmax re-bases only when a lane's P sum for a 64-key tile passes 2^15: keys whose
+    scores climb tile after tile ("up": +~6 log2 units per tile), a single huge-score key late in the
+    sequence ("spike": P would overflow fp16 without the re-base) and falling scores ("down": the
+    first tile's reference stays, later P underflow towards 0) all match torch fp32."""
+    B, N, H, D = 2, 600, 2, 64
+    g = torch.Generator().manual_seed(7)
+    q = torch.randn(B, N, H, D, generator=g)
+    k = torch.randn(B, N, H, D, generator=g)
+    v = torch.randn(B, N, H, D, generator=g)
+    pos = torch.arange(N, dtype=torch.float32)[None, :, None, None]
+    q = q + 1.0  # a common direction u = (1, ..., 1): q.u ~ D for every query
+    if ramp == "up":  # + ~40 log2 units over the sequence (~4 per tile)
+        k = k + pos / N * 3.5
+    elif ramp == "spike":  # one key ~46 log2 units above the rest
+        k[:, 500] = 4.0
+    else:
+        k = k + (N - pos) / N * 3.5
+    qkv = torch.stack([q, k, v], 2).reshape(B * N, 3 * H * D).half().float()
+    y = ops.spatial_attention(h(qkv), B, N, H, D)
+    qq, kk, vv = qkv.reshape(B, N, 3, H, D).permute(2, 0, 3, 1, 4)
+    ref = ((qq @ kk.transpose(-1, -2)) * D ** -0.5).softmax(-1) @ vv
+    ref = ref.transpose(1, 2).reshape(B * N, H * D)
+    assert torch.isfinite(y.float()).all()
+    assert rel(y, ref) < 3e-3
+
+
 @pytest.mark.parametrize("B,T,S,D", [(1, 32, 37, 128), (1, 8, 10, 32), (2, 5, 9, 48), (1, 32, 20, 8), (1, 3, 4, 24)])
 def test_temporal_attention(B, T, S, D):
     H = 8
