@@ -31,6 +31,9 @@ extern "C" int vda_debug_timestamps(void* host) {
 #ifndef VDA_PH2  // phased GEMM main loop: 2 phases per K tile (32 MFMAs between barriers) instead of 4
 #define VDA_PH2 0
 #endif
+#ifndef VDA_EPI_LINE  // register epilogue: whole 128-B output lines per store instruction
+#define VDA_EPI_LINE 1
+#endif
 #ifndef VDA_EEXP  // register-epilogue timing experiments (1: no GELU, 2: no stores; results wrong)
 #define VDA_EEXP 0
 #endif
@@ -1170,6 +1173,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_erf(v[i][r]);
         }
       }
+      u32x4 o[2];
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp) {
         float a[4], c[4];
@@ -1182,15 +1186,43 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         typedef float f2v __attribute__((ext_vector_type(2)));
         const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
         const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
-        const u32x4 o = {__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
-                         __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+        o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                      __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+      }
+#if VDA_EPI_LINE
+      // whole 128-B lines per store: lanes mcol < 8 trade their pp = 1 piece for the pp = 0 piece of
+      // row mcol + 8 (DPP row_ror:8 swaps lanes l and l ^ 8 of each 16-lane row), so one store covers
+      // rows mcol & 7 (A) and the other rows 8 + (mcol & 7) (B), each row's 64 channels in one go
+      const bool lo8 = (mcol & 8) == 0;
+      u32x4 A, B;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned snd = lo8 ? o[1][k] : o[0][k];
+        const unsigned got = (unsigned)__builtin_amdgcn_mov_dpp((int)snd, 0x128, 0xF, 0xF, true);
+        A[k] = lo8 ? o[0][k] : got;
+        B[k] = lo8 ? got : o[1][k];
+      }
+      const unsigned rA = (unsigned)((wm * 128 + j * 16 + (mcol & 7)) * p.ldy * 2) + (lo8 ? cofs[0] : cofs[1]);
+      const unsigned rB = rA + (unsigned)(8 * p.ldy * 2);
 #if VDA_EEXP == 2
-        asm volatile("" :: "v"(o));
+      asm volatile("" :: "v"(A), "v"(B));
+      (void)ry; (void)rofs; (void)rA; (void)rB;
+#else
+      (void)rofs;
+      __builtin_amdgcn_raw_buffer_store_b128(A, ry, rA, 0, VDA_EPI_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(B, ry, rB, 0, VDA_EPI_STORE_AUX);
+#endif
+#else
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+#if VDA_EEXP == 2
+        asm volatile("" :: "v"(o[pp]));
         (void)ry; (void)rofs;
 #else
-        __builtin_amdgcn_raw_buffer_store_b128(o, ry, rofs + cofs[pp], 0, VDA_EPI_STORE_AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(o[pp], ry, rofs + cofs[pp], 0, VDA_EPI_STORE_AUX);
 #endif
       }
+#endif
     }
     TS(5);
     return;
