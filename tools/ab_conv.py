@@ -1,0 +1,97 @@
+"""In-process A/B of the decoder's big convs across libvda builds (tuning tool, not product code).
+
+usage: python tools/ab_conv.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes oc1,depth,rcu148]
+oc1:    output_conv1, 3x3 256 -> 128 on the x2 bilinear resize of a [32, 148, 148, 256] map (fused)
+depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
+rcu148: refinenet1 RCU conv, 3x3 256 -> 256 at 148^2 with pre-ReLU + ReLU
+Outputs compared bit-for-bit against the first library's.
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from vda_amd import _lib
+
+args = sys.argv[1:]
+rounds, shapes, libs = 5, ["oc1", "depth"], []
+i = 0
+while i < len(args):
+    if args[i] == "--rounds":
+        rounds = int(args[i + 1]); i += 2
+    elif args[i] == "--shapes":
+        shapes = args[i + 1].split(","); i += 2
+    else:
+        libs.append(args[i]); i += 1
+L = []
+for p in libs:
+    l = ctypes.CDLL(os.path.abspath(p)); _lib._declare(l); L.append(l)
+dev = "cuda"
+torch.manual_seed(0)
+st = torch.cuda.current_stream().cuda_stream
+
+
+def case(name):
+    if name == "oc1":
+        x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
+        w = (torch.randn(128, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
+        b = torch.randn(128, device=dev) * 0.1
+        y = torch.empty(32, 296, 296, 128, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1, bias=b.data_ptr())
+        fl = 2.0 * 32 * 296 * 296 * 128 * 2304
+
+        def run(l):
+            return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 128, 3, 1, 1, 0, 296, 296,
+                                ctypes.byref(e), None, 0, st)
+        return run, y, fl, [x, w, b, e]
+    if name == "rcu148":
+        x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
+        w = (torch.randn(256, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
+        b = torch.randn(256, device=dev) * 0.1
+        y = torch.empty(32, 148, 148, 256, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1, bias=b.data_ptr(), act=_lib.ACT_RELU)
+        fl = 2.0 * 32 * 148 * 148 * 256 * 2304
+
+        def run(l):
+            return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 256, 3, 1, 1, 1, 0, 0,
+                                ctypes.byref(e), None, 0, st)
+        return run, y, fl, [x, w, b, e]
+    x = (torch.randn(32, 296, 296, 128, device=dev) * 0.5).half()
+    w32 = torch.randn(32, 3, 3, 128, device=dev) * (9 * 128) ** -0.5
+    w1 = torch.cat([w32.half(), (w32 - w32.half().float()).half()], 0).contiguous()
+    b1, w2, b2 = torch.randn(32, device=dev) * 0.1, torch.rand(32, device=dev) * 0.2, torch.tensor([0.05], device=dev)
+    d = torch.empty(32, 518, 518, device=dev)
+    fl = 2.0 * 32 * 518 * 518 * 64 * 1152
+
+    def run(l):
+        ws = l.vda_depth_head_workspace(32, 296, 296, 128, 518, 518)
+        assert ws == 0, ws
+        return l.vda_depth_head(x.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), d.data_ptr(),
+                                None, 32, 296, 296, 128, 518, 518, st)
+    return run, d, fl, [x, w1, b1, w2, b2]
+
+
+for name in shapes:
+    run, y, fl, keep = case(name)
+    outs = []
+    for l in L:
+        assert run(l) == 0, l.vda_last_error()
+        torch.cuda.synchronize()
+        outs.append(y.clone())
+    same = [bool(torch.equal(outs[0], o)) or f"rel {float((o.float() - outs[0].float()).abs().sum() / outs[0].float().abs().sum()):.1e}"
+            for o in outs[1:]]
+    times = [[] for _ in L]
+    for r in range(rounds):
+        for li, l in enumerate(L):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                run(l)
+            e1.record()
+            torch.cuda.synchronize()
+            times[li].append(e0.elapsed_time(e1) / 3 * 1e3)
+    line = f"{name:6s}: " + " | ".join(f"{os.path.basename(os.path.dirname(p))}: med {statistics.median(t):7.1f}us min {min(t):7.1f}us "
+                                      f"{fl / statistics.median(t) / 1e6:6.1f}TF" for p, t in zip(libs, times))
+    print(line + f" | bit-identical {same}", flush=True)

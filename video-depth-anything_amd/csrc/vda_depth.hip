@@ -78,9 +78,16 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   static_assert(!DEPTH || NROW == 64, "depth tail: 64 weight rows");
   constexpr int NB = NROW / 32;                          // n-blocks per wave (2 for the depth tail)
   constexpr int CPX = SLAB / 8;                          // 16-B chunks per pixel per slab
-  constexpr int PSLOT = DNPIX * CPX;                     // 16-B slots of one patch slab
+  // LIN (the plain conv): the patch is linear in the pixel with the pixel stride padded to PSTR slots
+  // (10 for 64-channel slabs, 6 for 32: conflict-free for the ds_read_b128 lane groups at any pixel
+  // offset, brute-forced), so a tap moves every fragment read by one constant: per step the reads
+  // cost one address add per output row and the rest are immediates.  The depth-tail instantiations
+  // keep the XOR-swizzled dense layout (their LDS has no room for the padding).
+  constexpr bool LIN = !DEPTH;
+  constexpr int PSTR = LIN ? (CPX == 8 ? 10 : 6) : CPX;  // 16-B slots per patch pixel
+  constexpr int PSLOT = DNPIX * PSTR;                    // 16-B slots of one patch slab
   constexpr int PP = (PSLOT + 63) / 64;                  // 1-KiB DMA pieces per slab
-  constexpr int PBUF = PP * 64 * 8;                      // halfs per patch ring slot
+  constexpr int PBUF = (UPS ? PSLOT : PP * 64) * 8;      // halfs per patch ring slot
   constexpr int WROW = TPS * CPX;                        // slots per weight row per step
   constexpr int WSLOT = NROW * WROW;                     // 16-B slots of one weight step
   constexpr int WBUF = WSLOT * 8;                        // halfs
@@ -88,9 +95,9 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   constexpr int WPW = (WPCS + 7) / 8;                    // per wave (3 or 2; surplus waves duplicate)
   constexpr int ND = SLAB / 32;                          // MFMA k-depths per tap
   constexpr int WRING = 2;                               // weight ring
-  static_assert(!UPS || (CPX == 8 && 9 / TPS >= 2), "UPS: 64-channel slabs, >= 2 steps per unit");
-  constexpr int SPPW = 3;                                // UPS source pieces per wave (fixed count)
-  constexpr int SSLOT = UPS ? SPPW * 8 * 64 : 0;         // source slots: 1536 = 192 pixels x 8 chunks
+  static_assert(!UPS || 9 / TPS >= 2, "UPS: >= 2 steps per unit");
+  constexpr int SPPW = (192 * CPX + 511) / 512;          // UPS source pieces per wave (fixed count)
+  constexpr int SSLOT = UPS ? SPPW * 8 * 64 : 0;         // source slots: >= 192 pixels x CPX chunks
   __shared__ __attribute__((aligned(16))) h16 dsm[2 * PBUF + WRING * WBUF + SSLOT * 8 + 512];
   h16* patch = dsm;                                      // [2][PBUF]
   h16* wbuf = dsm + 2 * PBUF;                            // [WRING][WBUF]
@@ -111,6 +118,8 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   const int my_steps = my_units * SPU;
   const void* zero = (const void*)g_dz_page;
 
+  // a unit's coordinates are formed once (the divisions are scalar but long), not per DMA piece
+  struct Ud { int bt, y0, x0, slab, sy_lo, sx_lo, SR, SC; };
   auto tile_of_unit = [&](int u, int& bt, int& y0, int& x0) {
     const int t = blockIdx.x + (u / units_per_tile) * gridDim.x;
     const int tx = t % tiles_x;
@@ -121,17 +130,15 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     x0 = tx * DT;
   };
   // piece q of unit u's patch slab -> ring slot (u & 1)
-  auto dma_patch = [&](int u, int q) {
-    int bt, y0, x0;
-    tile_of_unit(u, bt, y0, x0);
-    const int slab = u % units_per_tile;
+  auto dma_patch = [&](int u, const Ud& ud, int q) {
+    const int bt = ud.bt, y0 = ud.y0, x0 = ud.x0, slab = ud.slab;
     const int s = q * 64 + lane;
-    const int p = s / CPX, pos = s - p * CPX;
-    const int cd = patch_pos<CPX>(p, pos);
+    const int p = s / PSTR, pos = s - p * PSTR;
+    const int cd = LIN ? pos : patch_pos<CPX>(p, pos);
     const int pr = p / DP;
     const int py = y0 - 1 + pr, px = x0 - 1 + (p - pr * DP);
     const void* src = zero;
-    if (p < DNPIX && (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W)
+    if (p < DNPIX && pos < CPX && (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W)
       src = U + (((long)bt * H + py) * W + px) * C + slab * SLAB + cd * 8;
     dh_glds16(src, patch + (u & 1) * PBUF + q * 512);
   };
@@ -146,31 +153,34 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     SR = min((int)(usy * (float)min(y0 + DT, H - 1)) + 1, Hs - 1) - sy_lo + 1;
     SC = min((int)(usx * (float)min(x0 + DT, W - 1)) + 1, Ws - 1) - sx_lo + 1;
   };
-  // piece j (of SPPW) of unit u's source region -> sbuf; slot = pixel * 8 + chunk
-  auto dma_src = [&](int u, int j) {
-    int bt, y0, x0, sy_lo, sx_lo, SR, SC;
-    tile_of_unit(u, bt, y0, x0);
-    src_region(y0, x0, sy_lo, sx_lo, SR, SC);
-    const int slab = u % units_per_tile;
+  auto make_ud = [&](int u) {
+    Ud ud;
+    tile_of_unit(u, ud.bt, ud.y0, ud.x0);
+    ud.slab = u % units_per_tile;
+    ud.sy_lo = ud.sx_lo = ud.SR = ud.SC = 0;
+    if constexpr (UPS) src_region(ud.y0, ud.x0, ud.sy_lo, ud.sx_lo, ud.SR, ud.SC);
+    return ud;
+  };
+  // piece j (of SPPW) of unit u's source region -> sbuf; slot = pixel * CPX + chunk
+  auto dma_src = [&](const Ud& ud, int j) {
+    const int bt = ud.bt, sy_lo = ud.sy_lo, sx_lo = ud.sx_lo, SR = ud.SR, SC = ud.SC, slab = ud.slab;
     const int q = wave + j * 8;
     const int s = q * 64 + lane;
-    const int px = s >> 3, cd = s & 7;
+    const int px = s / CPX, cd = s % CPX;
     const int r = px / SC, c = px - r * SC;
     const void* src = zero;
     if (r < SR) src = U + (((long)bt * Hs + sy_lo + r) * Ws + sx_lo + c) * C + slab * SLAB + cd * 8;
     dh_glds16(src, sbuf + q * 512);
   };
   // interpolate unit u's patch from sbuf into patch ring slot (u & 1); padding pixels -> 0
-  auto ups_interp = [&](int u) {
-    int bt, y0, x0, sy_lo, sx_lo, SR, SC;
-    tile_of_unit(u, bt, y0, x0);
-    src_region(y0, x0, sy_lo, sx_lo, SR, SC);
+  auto ups_interp = [&](int u, const Ud& ud) {
+    const int y0 = ud.y0, x0 = ud.x0, sy_lo = ud.sy_lo, sx_lo = ud.sx_lo, SC = ud.SC;
 #pragma unroll
     for (int k = 0; k < UCH; ++k) {
       const int s = tid + k * 512;
       const int sc = min(s, USL - 1);
       const int p = sc / CPX, pos = sc - p * CPX;
-      const int cd = patch_pos<CPX>(p, pos);
+      const int cd = LIN ? pos : patch_pos<CPX>(p, pos);
       const int pr = p / DP;
       const int py = y0 - 1 + pr, px = x0 - 1 + (p - pr * DP);
       const bool ok = (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W;
@@ -179,19 +189,19 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       dh_ac_coord(min(max(py, 0), H - 1), Hs, usy, sy0, sy1, wy);
       dh_ac_coord(min(max(px, 0), W - 1), Ws, usx, sx0, sx1, wx);
       const int r0 = (sy0 - sy_lo) * SC, r1 = (sy1 - sy_lo) * SC, c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
-      const h8 a = *reinterpret_cast<const h8*>(sbuf + ((r0 + c0) * 8 + cd) * 8);
-      const h8 b = *reinterpret_cast<const h8*>(sbuf + ((r0 + c1) * 8 + cd) * 8);
-      const h8 c = *reinterpret_cast<const h8*>(sbuf + ((r1 + c0) * 8 + cd) * 8);
-      const h8 d = *reinterpret_cast<const h8*>(sbuf + ((r1 + c1) * 8 + cd) * 8);
+      const h8 a = *reinterpret_cast<const h8*>(sbuf + ((r0 + c0) * CPX + cd) * 8);
+      const h8 b = *reinterpret_cast<const h8*>(sbuf + ((r0 + c1) * CPX + cd) * 8);
+      const h8 c = *reinterpret_cast<const h8*>(sbuf + ((r1 + c0) * CPX + cd) * 8);
+      const h8 d = *reinterpret_cast<const h8*>(sbuf + ((r1 + c1) * CPX + cd) * 8);
       const h8 v = bilerp8(a, b, c, d, wx, wy);
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const uint4 o = ok ? __builtin_bit_cast(uint4, v) : z;
-      if (k + 1 < UCH || s < USL) *reinterpret_cast<uint4*>(patch + (u & 1) * PBUF + s * 8) = o;
+      const int slot = LIN ? p * PSTR + pos : s;
+      if (k + 1 < UCH || s < USL) *reinterpret_cast<uint4*>(patch + (u & 1) * PBUF + slot * 8) = o;
     }
   };
-  auto dma_w = [&](int gs) {
-    const int u = gs / SPU, st = gs - u * SPU;
-    const int slab = u % units_per_tile;
+  // weight pieces of step st of a unit of slab `slab` -> ring slot `wslot`
+  auto dma_w = [&](int st, int slab, int wslot) {
 #pragma unroll
     for (int j = 0; j < WPW; ++j) {
       const int piece = (wave * WPW + j) % WPCS;
@@ -199,27 +209,37 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       const int n = s / WROW, rem = s - n * WROW;
       const int tt = rem / CPX, pos = rem - tt * CPX;
       const int cd = w_pos<CPX>(n, pos);
-      dh_glds16(w1 + (long)n * K + (st * TPS + tt) * C + slab * SLAB + cd * 8, wbuf + (gs & 1) * WBUF + piece * 512);
+      dh_glds16(w1 + (long)n * K + (st * TPS + tt) * C + slab * SLAB + cd * 8, wbuf + wslot * WBUF + piece * 512);
     }
   };
 
   // prologue: patch of unit 0 (all pieces, split over waves) + weights of step 0
+  Ud ud_next = make_ud(0);
   if constexpr (UPS) {
-    for (int j = 0; j < SPPW; ++j) dma_src(0, j);
-    dma_w(0);
+    for (int j = 0; j < SPPW; ++j) dma_src(ud_next, j);
+    dma_w(0, ud_next.slab, 0);
     dh_wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    ups_interp(0);
+    ups_interp(0, ud_next);
     __syncthreads();  // patch slot 0 written, source slot free for unit 1
   } else {
-    for (int q = wave; q < PP; q += 8) dma_patch(0, q);
-    dma_w(0);
+    for (int q = wave; q < PP; q += 8) dma_patch(0, ud_next, q);
+    dma_w(0, ud_next.slab, 0);
     dh_wait_vmcnt<0>();
   }
   __builtin_amdgcn_s_barrier();
 
   const int frow = lane & 15, g = lane >> 4;
   const int jh = ng * 16 + g * 4;                        // this lane's 4 output channels (hi rows)
+  // LIN: lane-constant byte offsets of the fragment reads (output row i, k-depth d and the tap are
+  // immediates / one scalar per step); W rows keep their XOR swizzle, which depends on the row only
+  const unsigned lin_x = (unsigned)(((mg * 4) * DP + frow) * PSTR + g) * 16u;
+  unsigned lin_w[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const int n0r = (DEPTH ? ng : ng * NB) * 16 + frow;
+    lin_w[d] = (unsigned)(n0r * WROW + w_pos<CPX>(n0r, d * 4 + g)) * 16u;
+  }
   f4 acc[NB][4];
 #pragma unroll
   for (int a = 0; a < NB; ++a)
@@ -230,26 +250,61 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   float pend[4] = {0.f, 0.f, 0.f, 0.f};
   int pend_bt = -1, pend_y0 = 0, pend_x0 = 0;
 
+  // step counters kept incrementally (no per-step division): unit u, its step st and slab
+  int u = 0, st = 0, slab = 0;
   for (int gs = 0; gs < my_steps; ++gs) {
-    const int u = gs / SPU, st = gs - u * SPU;
     // weights of the next step first, then (first step of a unit) the whole next patch slab: the
     // end-of-step wait then leaves exactly the patch pieces in flight, and they land by the end of
     // the unit's second step
     const bool issue_p = st == 0 && u + 1 < my_units;
-    if (gs + 1 < my_steps) dma_w(gs + 1);
+    if (issue_p) ud_next = make_ud(u + 1);
+    if (gs + 1 < my_steps) {
+      if (st + 1 < SPU) dma_w(st + 1, slab, (gs + 1) & 1);
+      else dma_w(0, slab + 1 == nslab ? 0 : slab + 1, (gs + 1) & 1);
+    }
     if constexpr (UPS) {
       // first step: the next unit's source region (lands by the end of the second step); last step:
       // interpolate the next unit's patch from it into the other patch slot (published by this
       // step's barrier; the source slot is refilled only after it)
       if (issue_p)
-        for (int j = 0; j < SPPW; ++j) dma_src(u + 1, j);
-      if (st == SPU - 1 && u + 1 < my_units) ups_interp(u + 1);
+        for (int j = 0; j < SPPW; ++j) dma_src(ud_next, j);
+      if (st == SPU - 1 && u + 1 < my_units) ups_interp(u + 1, ud_next);
     } else if (issue_p) {
-      for (int j = 0; j < my_pp; ++j) dma_patch(u + 1, wave + j * 8);
+      for (int j = 0; j < my_pp; ++j) dma_patch(u + 1, ud_next, wave + j * 8);
     }
     // ---- TPS taps x ND k-depths x (NB x 4) MFMAs
     const h16* pb = patch + (u & 1) * PBUF;
     const h16* wb = wbuf + (gs & 1) * WBUF;
+    if constexpr (LIN) {
+      // one scalar per step: patch slot + this step's first tap offset, W slot (opaque: no strength
+      // reduction of the modulo counters into per-read VALU)
+      const int tap0 = st * TPS;
+      unsigned xs, ws;
+      asm volatile("s_mov_b32 %0, %1" : "=s"(xs)
+                   : "s"((unsigned)((u & 1) * PBUF * 2 + ((tap0 / 3) * DP + (tap0 % 3)) * PSTR * 16)));
+      asm volatile("s_mov_b32 %0, %1" : "=s"(ws) : "s"((unsigned)((gs & 1) * WBUF * 2)));
+      const char* pxb = reinterpret_cast<const char*>(patch) + xs + lin_x;
+      const char* wxb[ND];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) wxb[d] = reinterpret_cast<const char*>(wbuf) + ws + lin_w[d];
+#pragma unroll
+      for (int tt = 0; tt < TPS; ++tt) {  // taps of one step share the kernel row (TPS 3) or are one
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+          h8 wf[NB], xf[4];
+#pragma unroll
+          for (int a = 0; a < NB; ++a)
+            wf[a] = *reinterpret_cast<const h8*>(wxb[d] + ((DEPTH ? 2 * a : a) * 16 * WROW + tt * CPX) * 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            xf[i] = *reinterpret_cast<const h8*>(pxb + (i * DP + tt) * PSTR * 16 + d * 64);
+#pragma unroll
+          for (int a = 0; a < NB; ++a)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[a][i] = mfma16(wf[a], xf[i], acc[a][i]);
+        }
+      }
+    } else {
 #pragma unroll
     for (int tt = 0; tt < TPS; ++tt) {
       const int tap = st * TPS + tt;
@@ -274,7 +329,8 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
           for (int i = 0; i < 4; ++i) acc[a][i] = mfma16(wf[a], xf[i], acc[a][i]);
       }
     }
-    const bool tile_end = st == SPU - 1 && (u % units_per_tile) == units_per_tile - 1;
+    }
+    const bool tile_end = st == SPU - 1 && slab == units_per_tile - 1;
     if (!DEPTH && tile_end) {
       // +bias [ReLU] -> fp16 NHWC; lane: 4 consecutive channels of pixel (row mg*4+i, col frow)
       int bt, y0, x0;
@@ -337,6 +393,11 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
           if (y < H && x < W) depth[((long)pend_bt * H + y) * W + x] = fmaxf(v, 0.f);
         }
       }
+    }
+    if (++st == SPU) {
+      st = 0;
+      ++u;
+      if (++slab == nslab) slab = 0;
     }
   }
 }
