@@ -221,7 +221,9 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 // conflict-free for the b128 K reads and the b64 transposed V reads (brute-forced).
 // 152 VGPRs: three blocks per CU (3 x 48 KiB of LDS).  Measured and rejected (tools/ab_attn.py):
 // issuing the QK MFMAs of tile t+1 before the softmax of tile t (213 VGPRs, a 4-slot ring, two blocks
-// per CU) 333 vs 292 us; with the per-tile max still computed, 354 vs 320 us.
+// per CU) 333 vs 292 us; with the per-tile max still computed, 354 vs 320 us; each 32-key half of a
+// tile exponentiated, checked and multiplied into O on its own (so half 0's softmax can sit beside
+// half 1's QK MFMAs): 302 vs 297 us.
 // =============================================================================================
 constexpr int SA_KT = 64;    // keys per tile
 constexpr int SA_QB = 128;   // queries per block
