@@ -64,8 +64,11 @@ typedef struct vda_epilogue {
    * row stream x, W holds gamma (.) W_ln, bias holds W_ln beta + b, ln_colsum[n] = sum_k W[n, k] (of the
    * fp16 W actually used), and ln_stats[m] = (mean, rstd) of row m from vda_row_stats.  Then
    * rstd (x W^T - mean colsum) + bias = LN(x) W_ln^T + b exactly in real arithmetic.  ln_stats holds
-   * an even number of rows (M rounded up to 2).  Row store only, no gamma / rowbias, activation
-   * none / gelu. */
+   * an even number of rows (M rounded up to 2).  Row store only, no gamma, activation none / gelu.
+   * With a rowbias (the motion-module q/k/v: LN(x) + pe[t] then to_q/k/v, motion_module.py:175,256,
+   * 263): bias required, no activation / res / res2 / stats_out, rdiv >= 256, N % 256 == 0,
+   * M >= 4096, K % 64 == 0, 16-byte aligned x / y rows (the phased route's EK 3 epilogue; -22
+   * otherwise). */
   const float* ln_stats;  /* [round_up(M, 2), 2] or NULL                              */
   const float* ln_colsum; /* [N]                                                     */
   /* ln_parts > 0: ln_stats instead holds [M, ln_parts, 2] partial (sum, sum of squares) of row m

@@ -563,6 +563,52 @@ def test_gemm_layernorm_fold(M, N, K, act):
     assert err < max(2 * err0, 2e-3)
 
 
+@pytest.mark.parametrize("C,S,T,B", [(256, 300, 8, 2), (1024, 361, 4, 3), (256, 1369, 5, 1), (256, 256, 16, 1)])
+def test_gemm_layernorm_fold_rowbias(C, S, T, B):
+    """Motion-module q/k/v with its LayerNorm folded (motion_module.py:175, the EK 3 register epilogue):
+    rstd (x W'^T - mean colsum) + W beta + the frame's PE row bias pe[t] W^T (t = (row / S) % T), the
+    statistics as [M, P, 2] partials the producing GEMM writes; S = 300 / 361 put frame boundaries
+    inside 256-row tiles (two PE rows per tile), B > 1 wraps t, S = 256 aligns them.  vs torch fp32
+    LayerNorm -> + pe -> Linear, and vs the unfused route (LayerNorm kernel + row-bias GEMM)."""
+    M, N = B * T * S, 3 * C
+    g = torch.Generator().manual_seed(C + S + T)
+    x = (torch.randn(M, C, generator=g) * 2 + torch.randn(M, 1, generator=g)).half().float()
+    gam, bet = 1 + 0.2 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    w = torch.randn(N, C, generator=g) * C ** -0.5
+    pe = torch.randn(T, C, generator=g) * 0.5
+    t = (torch.arange(M) // S) % T
+    ref = F.linear(F.layer_norm(x, (C,), gam, bet, eps=1e-5) + pe[t], w)
+    rb = f32(pe @ w.t())
+    P = C // 256
+    xf = x.view(M, P, 256)
+    parts = torch.zeros(M + 1, P, 2)
+    parts[:M, :, 0], parts[:M, :, 1] = xf.sum(2), (xf * xf).sum(2)
+    wg = (w * gam[None, :]).half()
+    y = ops.gemm(h(x), wg.to(DEV), bias=f32(w @ bet), rowbias=rb, rdiv=S, rmod=T, ln_stats=f32(parts), ln_parts=P,
+                 ln_eps=1e-5, ln_colsum=f32(wg.float().sum(1)))
+    y0 = ops.gemm(ops.layernorm(h(x), f32(gam), f32(bet), 1e-5), h(w), rowbias=rb, rdiv=S, rmod=T)
+    err, err0 = rel(y, ref), rel(y0, ref)
+    print(f"LN-folded row-bias GEMM C={C} S={S} T={T} B={B}: rel-L1 {err:.2e} (unfused {err0:.2e})")
+    assert err < max(2 * err0, 2e-3)
+
+
+def test_gemm_layernorm_fold_rowbias_rejected_shapes():
+    """LN fold + row bias exists on the phased route only: frames shorter than a tile (rdiv < 256)
+    and N % 256 != 0 are rejected up front instead of running un-normalised."""
+    from vda_amd import _lib
+    lib = _lib.lib()
+    x = torch.zeros(8192, 256, dtype=torch.float16, device=DEV)
+    w = torch.zeros(768, 256, dtype=torch.float16, device=DEV)
+    y = torch.empty(8192, 768, dtype=torch.float16, device=DEV)
+    f = torch.zeros(8192 * 4, device=DEV)
+    e = Epilogue(rdiv=100, rmod=8, bias=f.data_ptr(), rowbias=f.data_ptr(), ln_stats=f.data_ptr(),
+                 ln_colsum=f.data_ptr(), ln_parts=1, ln_eps=1e-5)
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.vda_gemm(x.data_ptr(), 256, w.data_ptr(), y.data_ptr(), 768, 8192, 768, 256, e, st) == -22
+    e.rdiv = 300
+    assert lib.vda_gemm(x.data_ptr(), 256, w.data_ptr(), y.data_ptr(), 720, 8192, 720, 256, e, st) == -22
+
+
 @pytest.mark.parametrize("Cin,H,W,BT,mode", [(256, 148, 148, 2, "rcu2"), (256, 148, 148, 2, "rcu1"), (256, 74, 74, 3, "plain"),
                                              (64, 9, 33, 2, "rcu2"), (128, 17, 40, 1, "rcu1"), (512, 8, 32, 2, "plain"),
                                              (64, 1, 1, 3, "rcu2"), (256, 37, 150, 1, "rcu2")])

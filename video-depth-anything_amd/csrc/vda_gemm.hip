@@ -707,12 +707,13 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   static_assert(!(LNF && (ROWB || CONV)), "LNF: dense, no row bias");
   static_assert(EK == 0 || (!CONV && !ROWB), "fixed epilogue kinds: dense, no row bias");
   static_assert(EK != 2 || (ACT == VDA_ACT_NONE && !LNF), "EK 2: no activation, no LN fold");
+  static_assert(EK != 3 || (ACT == VDA_ACT_NONE && LNF), "EK 3: LN fold + per-frame row bias, no activation");
   const bool has_bias = EK ? true : p.epi.bias != nullptr;
   const bool has_gamma = EK ? false : p.epi.gamma != nullptr;
   const bool rows_store = EK ? true : p.epi.store == VDA_STORE_ROWS;
-  const bool has_res = EK == 2 ? true : EK == 1 ? false : p.epi.res != nullptr;
+  const bool has_res = EK == 2 ? true : (EK == 1 || EK == 3) ? false : p.epi.res != nullptr;
   const bool has_res2 = EK ? false : p.epi.res2 != nullptr;
-  const bool has_stats = EK == 2 ? true : EK == 1 ? false : p.epi.stats_out != nullptr;
+  const bool has_stats = EK == 2 ? true : (EK == 1 || EK == 3) ? false : p.epi.stats_out != nullptr;
   static_assert(XR * WR == 4 && (XR == 2 || XR == 4), "8 waves as XR (m) x 8/XR (n), wave tile 128 x 64");
   constexpr int BM = 128 * XR, BN = 128 * WR;
   constexpr int HALF = 128 * BK;            // halfs per 128-row region (16 KiB)
@@ -891,7 +892,20 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   const int wrow0 = (wn & 1) * 64;
 
   // prologue: [Phi table,] all of tile 0, then the two tile-1 quarters the loop expects from "tile -1"
-  auto lnst_dma = [&](int m0_) {
+  // EK 3: the tile's (at most two) per-frame row-bias rows, 256 fp32 channels each, after the
+  // statistics, in two slots by the parity of the block's tile index (a chaining epilogue stages the
+  // next tile's rows while it still reads its own)
+  float* rb_lds = reinterpret_cast<float*>(lnst_lds + 4096);
+  auto lnst_dma = [&](int m0_, int n0_, int vb_) {
+    if constexpr (EK == 3) {
+      if (wave < 2) {  // row 0 = the frame of tile row 0, row 1 = the next frame (rdiv >= 256: <= 2 per tile)
+        const int rd = p.epi.rdiv;
+        const int mrow = wave == 0 ? m0_ : min(m0_ + rd - m0_ % rd, p.M - 1);
+        const int t = (mrow / rd) % p.epi.rmod;
+        glds16(p.epi.rowbias + (long)t * p.N + n0_ + lane * 4,
+               reinterpret_cast<h16*>(rb_lds + ((vb_ / (int)gridDim.x) & 1) * 512) + wave * 512);
+      }
+    }
     if constexpr (LNF) {
       if (p.epi.ln_parts <= 0) {  // rows m0 .. m0+255 of [M, 2] fp32 (mean, rstd): 2 pieces of 128 rows, waves 0-1
         if (wave < 2) {
@@ -913,7 +927,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       glds16(src, smem + 2 * BUF + wave * 512);
       glds16(src + 8192, smem + 2 * BUF + 4096 + wave * 512);
     }
-    lnst_dma(m0);
+    lnst_dma(m0, n0, vb);
     TS(1);
     stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
     if (!PH2 && nk > 1) {
@@ -1097,7 +1111,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   TS(3);
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
-  if constexpr (EK == 1 && XR == 2 && WR == 2) {
+  if constexpr ((EK == 1 || EK == 3) && XR == 2 && WR == 2) {
     // Register epilogue (qkv, fc1): no LDS staging.  The LN statistics of the lane's 8 rows come out of
     // LDS first; then one barrier frees the operand buffers and the next tile's prologue DMA goes out
     // at once, landing under this tile's activation work and stores.  Pairs of accumulators (channels
@@ -1105,6 +1119,8 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     // lane holds 8 consecutive channels of its row: one 16-byte store per pair (16 rows x 64 B per wave
     // instruction; the two pairs of a row fill its 128-B line).
     const vda_epilogue& e = p.epi;
+    const int rbslot = (vb / (int)gridDim.x) & 1;
+    const int rbnd = EK == 3 ? e.rdiv - m0 % e.rdiv : 0;  // first tile row of the next frame
     float2 mr[8];
     if constexpr (LNF) {
       const float* st = reinterpret_cast<const float*>(lnst_lds);
@@ -1136,7 +1152,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
         unsigned xn[XR][2], wn2[WR][2];
         dense_offsets(tmn * BM, tnn * BN, xn, wn2);
-        lnst_dma(tmn * BM);
+        lnst_dma(tmn * BM, tnn * BN, vb_next);
         chain_dma(xn, wn2);
       }
     }
@@ -1164,6 +1180,10 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           for (int r = 0; r < 4; ++r) v[i][r] = fmaf(mr[j].y, fmaf(-mr[j].x, pgv[i][r], v[i][r]), pbv[i][r]);
         } else {
           v[i] += pbv[i];
+        }
+        if constexpr (EK == 3) {  // + the row's frame PE row bias (slot row 1 past the frame boundary)
+          const int rl = wm * 128 + j * 16 + mcol;
+          v[i] += *reinterpret_cast<const f4*>(rb_lds + rbslot * 512 + (rl >= rbnd ? 256 : 0) + wn * 64 + i * 16 + nq);
         }
         if constexpr (ACT == VDA_ACT_GELU && TAB && VDA_EEXP != 1) {
 #pragma unroll
@@ -1524,7 +1544,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         tile_coords(vb_next, tiles_m * tiles_n, tiles_m, tiles_n, tmn, tnn);
         unsigned xn[XR][2], wn2[WR][2];
         dense_offsets(tmn * BM, tnn * BN, xn, wn2);
-        lnst_dma(tmn * BM);
+        lnst_dma(tmn * BM, tnn * BN, vb_next);
         chain_dma(xn, wn2);
       }
     }
@@ -1641,7 +1661,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
   __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0) +
-                                                     (EK == 2 ? 4096 : 0)];
+                                                     (EK == 2 ? 4096 : 0) + (EK == 3 ? 2048 : 0)];
   const int ntiles = tiles_m * tiles_n;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
@@ -1720,6 +1740,13 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
   int grid, ticks;
   phased_sched(tiles_m * tiles_n, (p.K + 63) / 64, CONV, grid, ticks);
+  if constexpr (!CONV && ACT == VDA_ACT_NONE && XR == 2) {
+    if (p.epi.rowbias && p.epi.ln_stats) {  // LN fold + per-frame row bias (motion-module q/k/v), EK 3
+      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false, true, 3>), dim3(grid), dim3(512), 0, st, p, tiles_m,
+                         tiles_n, ticks, g_desync);
+      return;
+    }
+  }
   if constexpr (!CONV && ACT == VDA_ACT_NONE) {
     if (p.epi.rowbias) {
       hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n, ticks,
@@ -1854,11 +1881,15 @@ int check_epi(const vda_epilogue& e, int N) {
                 (e.store == VDA_STORE_PIXEL_SHUFFLE && e.ps_k > 0 && e.ps_cout > 0 && e.ps_cout % 4 == 0 &&
                  e.ps_hin > 0 && e.ps_win > 0 && N == e.ps_k * e.ps_k * e.ps_cout && !e.res && !e.res2),
                 "bad pixel-shuffle store geometry");
-  // the LN fold exists for the activation-free and GELU epilogues without a row bias (every kernel
-  // route applies it there; anything else would silently run an un-normalised GEMM)
-  VDA_CHECK_ARG(!e.ln_stats || (e.ln_colsum && e.store == VDA_STORE_ROWS && !e.gamma && !e.rowbias &&
+  // the LN fold exists for the activation-free and GELU epilogues (every kernel route applies it
+  // there; anything else would silently run an un-normalised GEMM); with a row bias only on the
+  // phased route's EK 3 epilogue (vda_gemm checks the shape)
+  VDA_CHECK_ARG(!e.ln_stats || (e.ln_colsum && e.store == VDA_STORE_ROWS && !e.gamma &&
                                  (e.act == VDA_ACT_NONE || e.act == VDA_ACT_GELU)),
-                "ln_stats needs ln_colsum, a row store, no gamma / rowbias, activation none / gelu");
+                "ln_stats needs ln_colsum, a row store, no gamma, activation none / gelu");
+  VDA_CHECK_ARG(!e.ln_stats || !e.rowbias ||
+                    (e.act == VDA_ACT_NONE && e.bias && !e.res && !e.res2 && !e.stats_out && e.rdiv >= 256),
+                "ln_stats with rowbias needs a bias, no activation / residual / stats_out, rdiv >= 256");
   VDA_CHECK_ARG(!e.ln_stats || (e.ln_parts >= 0 && e.ln_parts <= 4), "ln_parts must be 0 .. 4");
   VDA_CHECK_ARG(!e.stats_out || (e.store == VDA_STORE_ROWS && e.act != VDA_ACT_GEGLU),
                 "stats_out needs a row store and no GEGLU");
@@ -1883,6 +1914,12 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
   int rc = check_epi(p.epi, N);
   if (rc) return rc;
+  if (p.epi.ln_stats && p.epi.rowbias) {  // only the phased 256x256 route (EK 3) implements the pair
+    const bool a16 = ((uintptr_t)p.y % 16 == 0) && ldy % 8 == 0 && ((uintptr_t)p.x % 16 == 0);
+    VDA_CHECK_ARG(N % 256 == 0 && M >= 4096 && K % 64 == 0 && a16 && (long)M * ldx * 2 < (1L << 31) &&
+                      (long)N * K * 2 < (1L << 31) && g_force_tile == -1,
+                  "ln_stats with rowbias needs N % 256 == 0, M >= 4096, K % 64 == 0, 16-B aligned rows");
+  }
   return launch<false>(p, (hipStream_t)stream);
 }
 

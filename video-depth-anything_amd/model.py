@@ -398,6 +398,13 @@ class VideoDepthAnything(nn.Module):
                 # temporal attention kernel instead (motion_module.py:290-293).
                 a.pe_bias = (_f(ab.pos_encoder.pe[0].float() @ wqkv.t()).to(dev)  # [max_len, 3C]
                              if ab.pos_encoder is not None else None)
+                # the LayerNorm folded into that GEMM (fp16, 'ape'; the forward takes it when a frame
+                # spans >= 256 rows): W' = gamma (.) W, colsum of the fp16 W', b' = W beta
+                a.fold = not fp32 and a.pe_bias is not None and (3 * Cm) % 256 == 0
+                if a.fold:
+                    a.qkv_wg = (wqkv * nrm.weight.detach().float()[None, :]).half().contiguous().to(dev)
+                    a.qkv_cs = a.qkv_wg.float().sum(1).contiguous()
+                    a.qkv_bb = (wqkv @ nrm.bias.detach().float()).contiguous().to(dev)
                 a.out_w, a.out_b = _h(ab.to_out[0].weight).to(dev), _f(ab.to_out[0].bias).to(dev)
                 q.attn.append(a)
             q.ffnw, q.ffnb = _f(blk.ff_norm.weight).to(dev), _f(blk.ff_norm.bias).to(dev)
@@ -445,19 +452,31 @@ class VideoDepthAnything(nn.Module):
 
     # -- forward ---------------------------------------------------------------------------
     def _temporal(self, q: _Packed, x: torch.Tensor, B: int, T: int, S: int) -> torch.Tensor:
-        """TemporalModule on token-major frames x [B*T*S, C] (motion_module.py:64-133)."""
+        """TemporalModule on token-major frames x [B*T*S, C] (motion_module.py:64-133).
+        The attention blocks' LayerNorms (motion_module.py:175) are folded into their q/k/v GEMMs when
+        a frame spans >= 256 rows (each 256-row tile then sees <= 2 PE rows): the GEMM producing the
+        residual stream h (proj_in, then each to_out) writes h's per-row partial sums."""
         C = q.C
+        M = x.shape[0]
         xn = ops.groupnorm(x, q.gnw, q.gnb, B * T, 32, 1e-6)
-        h = ops.gemm(xn, q.pin_w, bias=q.pin_b)
-        for a in q.attn:
-            n = ops.layernorm(h, a.nw, a.nb, 1e-5)
-            if a.pe_bias is not None:
-                qkv = ops.gemm(n, a.qkv_w, rowbias=a.pe_bias, rdiv=S, rmod=T)
+        fold = [a.fold and S >= 256 and M >= 4096 for a in q.attn]
+        st = torch.empty(M + 1, (C + 255) // 256, 2, device=x.device) if any(fold) else None
+        h = ops.gemm(xn, q.pin_w, bias=q.pin_b, stats_out=st if fold[0] else None)
+        for i, a in enumerate(q.attn):
+            if fold[i]:  # rstd (h W'^T - mean colsum) + W beta + pe[t] W^T
+                qkv = ops.gemm(h, a.qkv_wg, bias=a.qkv_bb, rowbias=a.pe_bias, rdiv=S, rmod=T, ln_stats=st,
+                               ln_parts=st.shape[1], ln_eps=1e-5, ln_colsum=a.qkv_cs)
                 at = ops.temporal_attention(qkv, B, T, S, 8, C // 8)
-            else:  # pe='rope': rotary q/k (theta 1e4, pairs over all C channels) in the attention kernel
-                qkv = ops.gemm(n, a.qkv_w)
-                at = ops.temporal_attention(qkv, B, T, S, 8, C // 8, rope_theta=10000.0)
-            h = ops.gemm(at, a.out_w, bias=a.out_b, res=h, out=h)
+            else:
+                n = ops.layernorm(h, a.nw, a.nb, 1e-5)
+                if a.pe_bias is not None:
+                    qkv = ops.gemm(n, a.qkv_w, rowbias=a.pe_bias, rdiv=S, rmod=T)
+                    at = ops.temporal_attention(qkv, B, T, S, 8, C // 8)
+                else:  # pe='rope': rotary q/k (theta 1e4, pairs over all C channels) in the attention kernel
+                    qkv = ops.gemm(n, a.qkv_w)
+                    at = ops.temporal_attention(qkv, B, T, S, 8, C // 8, rope_theta=10000.0)
+            nxt = i + 1 < len(q.attn) and fold[i + 1]
+            h = ops.gemm(at, a.out_w, bias=a.out_b, res=h, out=h, stats_out=st if nxt else None)
         n = ops.layernorm(h, q.ffnw, q.ffnb, 1e-5)
         g = ops.gemm(n, q.ff1_w, bias=q.ff1_b, act=ACT_GEGLU)
         h = ops.gemm(g, q.ff2_w, bias=q.ff2_b, res=h, out=h)
