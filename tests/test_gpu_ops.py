@@ -592,6 +592,27 @@ def test_gemm_layernorm_fold_rowbias(C, S, T, B):
     assert err < max(2 * err0, 2e-3)
 
 
+@pytest.mark.parametrize("M,N,K", [(5000, 1024, 512), (43808, 256, 256), (4001, 768, 256)])
+def test_gemm_row_stats_no_residual(M, N, K):
+    """stats_out on a GEMM without a residual (the motion modules' proj_in feeding the folded
+    LayerNorm): the phased epilogue writes the per-row partials itself (no separate pass) and they
+    equal torch sums of the stored fp16 values."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 0.5).half().float()
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    b = 0.1 * torch.randn(N, generator=g)
+    P = (N + 255) // 256
+    st = torch.full((M + 1, P, 2), float("nan"), device=DEV)
+    y = ops.gemm(h(x), h(w), bias=f32(b), stats_out=st)
+    yc = y.float().cpu()
+    pad = torch.zeros(M, P * 256)
+    pad[:, :N] = yc
+    stc = st[:M].cpu()
+    assert torch.allclose(stc[..., 0], pad.view(M, P, 256).sum(2), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(stc[..., 1], (pad * pad).view(M, P, 256).sum(2), rtol=1e-4, atol=1e-3)
+    assert rel(y, F.linear(x, w, b)) < 2e-3
+
+
 def test_gemm_layernorm_fold_rowbias_rejected_shapes():
     """LN fold + row bias exists on the phased route only: frames shorter than a tile (rdiv < 256)
     and N % 256 != 0 are rejected up front instead of running un-normalised."""

@@ -1579,27 +1579,39 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
       }
     };
+    // + per-row partial (sum, sumsq) of the stored values for a following LN fold (the stored tile
+    // values tv [+ the prefetched residual]): a half-wave per row, 16 rows per lane
+    auto store_with_stats = [&](auto with_res) {
+      constexpr bool WR1 = decltype(with_res)::value;
+      static_assert(NIT == 16 && RPI == 16, "stats: a half-wave per row, 16 rows per lane");
+      const bool cval = c < nout;
+      float v[32];
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        h8 t = tv[it];
+        if constexpr (WR1) t += rpre[it];
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
+        stat_acc(cval ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, v[it], v[16 + it]);
+      }
+      const float r = halfwave_sum32(v, lane);
+      const int P = (p.N + 255) / 256;
+      const int m = m0 + row0 + 16 * (lane & 15);
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)e.stats_out, (short)0, (int)((long)p.M * P * 8), 0x00020000);
+      const unsigned vo = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + ((lane >> 4) & 1)) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, vo, 0, 0);
+    };
     if (nres == 0) {
-      phase2(std::integral_constant<int, 0>{});
+      if constexpr (RPF) {
+        if (has_stats) store_with_stats(std::false_type{});
+        else phase2(std::integral_constant<int, 0>{});
+      } else {
+        phase2(std::integral_constant<int, 0>{});
+      }
     } else if (nres == 1) {
       if constexpr (RPF) {
-        if (has_stats) {  // + per-row partial (sum, sumsq) of the stored values for a following LN fold
-          static_assert(NIT == 16 && RPI == 16, "stats: a half-wave per row, 16 rows per lane");
-          const bool cval = c < nout;
-          float v[32];
-#pragma unroll
-          for (int it = 0; it < NIT; ++it) {
-            const h8 t = tv[it] + rpre[it];
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vy + it * sy, 0, VDA_EPI_STORE_AUX);
-            stat_acc(cval ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, v[it], v[16 + it]);
-          }
-          const float r = halfwave_sum32(v, lane);
-          const int P = (p.N + 255) / 256;
-          const int m = m0 + row0 + 16 * (lane & 15);
-          const __amdgpu_buffer_rsrc_t rs =
-              __builtin_amdgcn_make_buffer_rsrc((void*)e.stats_out, (short)0, (int)((long)p.M * P * 8), 0x00020000);
-          const unsigned vo = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + ((lane >> 4) & 1)) * 4) : 0x80000000u;
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, vo, 0, 0);
+        if (has_stats) {
+          store_with_stats(std::true_type{});
         } else {
 #pragma unroll
           for (int it = 0; it < NIT; ++it) {
@@ -1838,10 +1850,10 @@ int launch(const GemmParams& p, hipStream_t st) {
   }
   VDA_LAUNCH_CHECK();
   if (p.epi.stats_out) {
-    // the phased 256x256 dense activation-free kernel with exactly one residual writes the partial
+    // the phased 256x256 dense activation-free kernel with at most one residual writes the partial
     // row statistics in its epilogue; any other route gets them from a separate partial-sum pass
     const int nres = (p.epi.res ? 1 : 0) + (p.epi.res2 ? 1 : 0);
-    const bool in_epi = !CONV && cfg == 4 && p.epi.act == VDA_ACT_NONE && !p.epi.rowbias && !p.epi.ln_stats && nres == 1;
+    const bool in_epi = !CONV && cfg == 4 && p.epi.act == VDA_ACT_NONE && !p.epi.rowbias && !p.epi.ln_stats && nres <= 1;
     if (!in_epi) return vda_row_partials_launch(p.y, p.ldy, p.epi.stats_out, p.M, p.N, st);
   }
   return 0;
