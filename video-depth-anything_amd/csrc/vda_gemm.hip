@@ -28,18 +28,6 @@ extern "C" int vda_debug_timestamps(void* host) {
 #define TS(k) do {} while (0)
 #endif
 #include "../../include/vda.h"
-#ifndef VDA_PH2  // phased GEMM main loop: 2 phases per K tile (32 MFMAs between barriers) instead of 4
-#define VDA_PH2 0
-#endif
-#ifndef VDA_EPI_LINE  // register epilogue: whole 128-B output lines per store instruction
-#define VDA_EPI_LINE 1
-#endif
-#ifndef VDA_EEXP  // register-epilogue timing experiments (1: no GELU, 2: no stores; results wrong)
-#define VDA_EEXP 0
-#endif
-#ifndef VDA_GEXP  // main-loop timing experiments (tools/build_variants.sh; 0 = the kernel)
-#define VDA_GEXP 0
-#endif
 
 // cache policy of the phased epilogue's output stores: nt (aux = 2).  In-situ A/B on one box
 // (tools/ab_libs.sh, 2 rounds): every phased GEMM/conv class 0.7-3.6 % faster, the forward's kernel
@@ -875,14 +863,11 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
-  constexpr bool PH2 = VDA_PH2 != 0 && EK == 1;
   // the next tile's prologue, issued by a chaining epilogue: K tile 0 (and the two K-tile-1 quarters
   // the 4-phase loop expects from "tile -1")
   auto chain_dma = [&](const unsigned (&xn)[XR][2], const unsigned (&wn2)[WR][2]) {
     bdma_x(0, 0, 0, xn); bdma_x(0, 0, 1, xn); bdma_w(0, 0, 0, wn2); bdma_w(0, 0, 1, wn2);
-    if constexpr (!PH2) {
-      if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
-    }
+    if (nk > 1) { bdma_x(1, 1, 0, xn); bdma_w(1, 1, 1, wn2); }
   };
   const int frow = lane & 15, fchunk = lane >> 4;
   const bool prerelu = CONV && p.pre_relu;
@@ -930,7 +915,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     lnst_dma(m0, n0, vb);
     TS(1);
     stage_x(0, 0, 0); stage_x(0, 0, 1); stage_w(0, 0, 0); stage_w(0, 0, 1);
-    if (!PH2 && nk > 1) {
+    if (nk > 1) {
       stage_x(1, 1, 0); stage_w(1, 1, 1);
       wait_vmcnt<XR + WR>();
     } else {
@@ -938,7 +923,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     }
   } else {
     // issued by the previous tile's epilogue, followed by at least NIT_EPI output stores
-    if (!PH2 && nk > 1) wait_vmcnt<XR + WR + NIT_EPI>();
+    if (nk > 1) wait_vmcnt<XR + WR + NIT_EPI>();
     else wait_vmcnt<NIT_EPI>();
   }
   __builtin_amdgcn_s_barrier();
@@ -989,9 +974,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         wf[i][ks] = *reinterpret_cast<const h8*>(&base[woff + swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
   };
   auto mma = [&](int qm, int qn) {
-#if VDA_GEXP < 4
     __builtin_amdgcn_s_barrier();
-#endif
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -1004,68 +987,9 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           acc[qn * 2 + i][qm * 4 + j] = mfma16(wf[i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-#if VDA_GEXP < 3
     __builtin_amdgcn_s_barrier();
-#endif
   };
 
-  if constexpr (PH2) {
-    // Two phases per K tile, 32 MFMAs each: A = X rows q0 x all 64 W columns, B = X rows q1 x the same
-    // W fragments (held in registers across both).  A barrier interval (one wave per SIMD in its MFMA
-    // segment, the other reading LDS / issuing DMA) then spans 512 MFMA cycles instead of 256, halving
-    // the barrier count per K tile.  DMA: K tile t+1 goes into the other buffer, W + X q0 in A(t),
-    // X q1 in B(t), each >= 2 intervals after that region's last read (lagging waves included) and
-    // retired two intervals after issue, before the barrier that precedes its first read.
-    h8 wg[2][2][2];
-    auto load_w2 = [&](const h16* base, int qn) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          wg[qn][i][ks] = *reinterpret_cast<const h8*>(&base[woff + swz(wrow0 + qn * 32 + i * 16 + frow, ks * 4 + fchunk)]);
-    };
-    auto mma2 = [&](int qm) {
-      __builtin_amdgcn_s_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int qn = 0; qn < 2; ++qn)
-#pragma unroll
-          for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[qn * 2 + i][qm * 4 + j] = mfma16(wg[qn][i][ks], xf[j][ks], acc[qn * 2 + i][qm * 4 + j]);
-      __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
-    };
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cb = kt & 1, nb = cb ^ 1;
-      const h16* base = smem + cb * BUF;
-      const bool more1 = kt + 1 < nk;
-      // A: also retires X q1 of this tile (issued in B(t-1))
-      load_x(base, 0);
-      load_w2(base, 0);
-      load_w2(base, 1);
-      if (more1) {
-        stage_w(kt + 1, nb, 0); stage_w(kt + 1, nb, 1); stage_x(kt + 1, nb, 0);
-        wait_vmcnt<2 * WR + XR>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      mma2(0);
-      // B: retires W + X q0 of tile t+1
-      load_x(base, 1);
-      if (more1) {
-        stage_x(kt + 1, nb, 1);
-        wait_vmcnt<XR>();
-      }
-      mma2(1);
-    }
-  } else
   // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
   // and retired by the P4 wait one phase before its first read:
   //   P1: Xq1(t+1) -> other buffer   P2: Wq0(t+1) -> other   P3: Xq0(t+2) -> this   P4: Wq1(t+2) -> this
@@ -1073,38 +997,27 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     const int cb = kt & 1, nb = cb ^ 1;
     const h16* base = smem + cb * BUF;
     const bool more1 = kt + 1 < nk, more2 = kt + 2 < nk;
-#if VDA_GEXP >= 2  // timing experiments only (results wrong): no operand DMA in the loop
-    (void)more1; (void)more2; (void)nb;
-#define VDA_STAGE(...) do {} while (0)
-#else
-#define VDA_STAGE(...) __VA_ARGS__
-#endif
     // P1
     load_x(base, 0);
     load_w(base, 0);
-    if (more1) VDA_STAGE(stage_x(kt + 1, nb, 1));
+    if (more1) stage_x(kt + 1, nb, 1);
     mma(0, 0);
     // P2
     load_w(base, 1);
-    if (more1) VDA_STAGE(stage_w(kt + 1, nb, 0));
+    if (more1) stage_w(kt + 1, nb, 0);
     mma(0, 1);
     // P3
     load_x(base, 1);
-    if (more2) VDA_STAGE(stage_x(kt + 2, cb, 0));
+    if (more2) stage_x(kt + 2, cb, 0);
     mma(1, 1);
     // P4: retire everything but this tile's two P3/P4 quarters
     load_w(base, 0);
-#if VDA_GEXP == 0
     if (more2) {
       stage_w(kt + 2, cb, 1);
       wait_vmcnt<XR + WR>();
     } else {
       wait_vmcnt<0>();
     }
-#elif VDA_GEXP == 1
-    if (more2) stage_w(kt + 2, cb, 1);
-#endif
-#undef VDA_STAGE
     mma(1, 0);
   }
   if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
@@ -1116,8 +1029,9 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     // LDS first; then one barrier frees the operand buffers and the next tile's prologue DMA goes out
     // at once, landing under this tile's activation work and stores.  Pairs of accumulators (channels
     // 16i.. and 16(i+1)..) are exchanged across 16-lane rows with v_permlane16_swap, after which every
-    // lane holds 8 consecutive channels of its row: one 16-byte store per pair (16 rows x 64 B per wave
-    // instruction; the two pairs of a row fill its 128-B line).
+    // lane holds 8 consecutive channels of its row; a DPP row_ror:8 exchange between lanes l and l ^ 8
+    // then lets each 16-byte-per-lane store write 8 whole 128-B lines.  EK 3 (the motion-module q/k/v)
+    // adds the row's frame PE row bias from the two rows staged in LDS.
     const vda_epilogue& e = p.epi;
     const int rbslot = (vb / (int)gridDim.x) & 1;
     const int rbnd = EK == 3 ? e.rdiv - m0 % e.rdiv : 0;  // first tile row of the next frame
@@ -1170,7 +1084,6 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const unsigned rofs = (unsigned)((wm * 128 + j * 16 + mcol) * p.ldy * 2);
       f4 v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -1185,10 +1098,10 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           const int rl = wm * 128 + j * 16 + mcol;
           v[i] += *reinterpret_cast<const f4*>(rb_lds + rbslot * 512 + (rl >= rbnd ? 256 : 0) + wn * 64 + i * 16 + nq);
         }
-        if constexpr (ACT == VDA_ACT_GELU && TAB && VDA_EEXP != 1) {
+        if constexpr (ACT == VDA_ACT_GELU && TAB) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_tab(v[i][r], phib);
-        } else if constexpr (ACT == VDA_ACT_GELU && VDA_EEXP != 1) {
+        } else if constexpr (ACT == VDA_ACT_GELU) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_erf(v[i][r]);
         }
@@ -1209,10 +1122,10 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
                       __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
       }
-#if VDA_EPI_LINE
       // whole 128-B lines per store: lanes mcol < 8 trade their pp = 1 piece for the pp = 0 piece of
       // row mcol + 8 (DPP row_ror:8 swaps lanes l and l ^ 8 of each 16-lane row), so one store covers
       // rows mcol & 7 (A) and the other rows 8 + (mcol & 7) (B), each row's 64 channels in one go
+      // (64-B half lines measured 430 MB of WRITE_SIZE for fc1's 359 MB of output)
       const bool lo8 = (mcol & 8) == 0;
       u32x4 A, B;
 #pragma unroll
@@ -1224,25 +1137,8 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       }
       const unsigned rA = (unsigned)((wm * 128 + j * 16 + (mcol & 7)) * p.ldy * 2) + (lo8 ? cofs[0] : cofs[1]);
       const unsigned rB = rA + (unsigned)(8 * p.ldy * 2);
-#if VDA_EEXP == 2
-      asm volatile("" :: "v"(A), "v"(B));
-      (void)ry; (void)rofs; (void)rA; (void)rB;
-#else
-      (void)rofs;
       __builtin_amdgcn_raw_buffer_store_b128(A, ry, rA, 0, VDA_EPI_STORE_AUX);
       __builtin_amdgcn_raw_buffer_store_b128(B, ry, rB, 0, VDA_EPI_STORE_AUX);
-#endif
-#else
-#pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-#if VDA_EEXP == 2
-        asm volatile("" :: "v"(o[pp]));
-        (void)ry; (void)rofs;
-#else
-        __builtin_amdgcn_raw_buffer_store_b128(o[pp], ry, rofs + cofs[pp], 0, VDA_EPI_STORE_AUX);
-#endif
-      }
-#endif
     }
     TS(5);
     return;
