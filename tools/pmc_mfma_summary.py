@@ -16,7 +16,8 @@ from collections import defaultdict
 # <XR, WR, CONV, ACT, ROWB, LNF, EK>; ACT 1 = GELU; LNF = LayerNorm folded into the epilogue.
 TAGS = [
     (r"^gemm256_kernel<2, 2, false, 1, false, true\b", "enc_fc1"),            # norm2 + fc1 + GELU (register epilogue)
-    (r"^gemm256_kernel<2, 2, false, 0, false, true\b", "enc_qkv"),            # norm1 + qkv (register epilogue)
+    (r"^gemm256_kernel<2, 2, false, 0, false, true, 1>", "enc_qkv"),          # norm1 + qkv (register epilogue)
+    (r"^gemm256_kernel<2, 2, false, 0, false, true, 3>", "mm_qkv_lnfold"),    # motion-module LN + q/k/v + PE
     (r"^gemm256_kernel<2, 2, false, 0, false, false, 0>", "gemm_staged"),      # proj / fc2 (+ residual, row stats) and others
     (r"^gemm256_kernel<2, 2, false, 0, false, false, 1>", "gemm_bias_rows"),
     (r"^gemm256_kernel<2, 2, false, 0, true\b", "gemm_rowbias"),
