@@ -85,6 +85,12 @@ typedef struct vda_epilogue {
    * shape does not take the phased 256x256 kernel (then N % 8 == 0, ldy % 8 == 0, y 16-byte aligned).
    * Not available in the fp32 entry points. */
   float* stats_out;
+  /* res2_h, res2_w > 0 (vda_conv2d only): res2 is a smaller [BT, res2_h, res2_w, N] map read through a
+   * bilinear align_corners=True upsample to the output grid (the FeatureFusionBlock input upsampled by
+   * the previous block, blocks.py:156-158, consumed as refinenet1's skip add, blocks.py:146-150),
+   * bit-identical to vda_upsample_bilinear + the add; ldres2 is then the source row stride (= N).
+   * Served where vda_conv2d_res2_upsample_ok says so (the halo-tiled 256-channel conv); 0 = same grid. */
+  int32_t res2_h, res2_w;
 } vda_epilogue;
 
 /* Version / diagnostics. */
@@ -128,6 +134,10 @@ int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int
                void* ws, int64_t ws_bytes, void* stream);
 int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
                              int32_t stride, int32_t pad);
+/* 1 when vda_conv2d of this shape takes an epilogue res2 through the fused upsample (res2_h/res2_w),
+ * else 0 (the caller materialises the upsample with vda_upsample_bilinear instead). */
+int vda_conv2d_res2_upsample_ok(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
+                                int32_t stride, int32_t pad);
 
 /*
  * Row LayerNorm, fp32 statistics.  X rows of C halfs (row stride ldx); Y [rows, C] half.

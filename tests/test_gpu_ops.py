@@ -665,6 +665,47 @@ def test_conv3x3_hconv_cout256(Cin, H, W, BT, mode):
     assert rel(y, y2) < 1e-3
 
 
+@pytest.mark.parametrize("BT,Cin,Hs,Ws,H,W", [(2, 256, 74, 74, 148, 148), (1, 256, 74, 132, 148, 264),
+                                              (2, 64, 5, 17, 9, 33), (1, 128, 40, 12, 79, 23)])
+def test_conv3x3_hconv_res2_upsample(BT, Cin, Hs, Ws, H, W):
+    """refinenet1's RCU conv2 (blocks.py:146-150) with its skip input res2 = refinenet2's output read
+    through the bilinear align_corners=True upsample (blocks.py:156-158) in the halo conv's epilogue:
+    bit-identical to vda_upsample_bilinear + the same conv, vs torch fp32; the op materialises the
+    upsample where the conv route has no such epilogue (same bits on that route)."""
+    x = rnd(BT, Cin, H, W, seed=300)
+    w, b = rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=301), rnd(256, scale=0.1, seed=302)
+    r1, r2 = rnd(BT, 256, H, W, seed=303), rnd(BT, 256, Hs, Ws, seed=304)
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    xh, wh, r1h, r2h = nh(x), nh(w), nh(r1), nh(r2)
+    up = ops.upsample_bilinear(r2h, H, W)
+    ref = F.conv2d(x, w, b, padding=1) + r1 + F.interpolate(r2, size=(H, W), mode="bilinear", align_corners=True)
+    T = tune_lib()
+    with T.route(hconv=1):
+        assert T.lib.vda_conv2d_res2_upsample_ok(BT, H, W, Cin, 256, 3, 1, 1) == 1
+        y = T.conv2d(xh, wh, bias=f32(b), res=r1h, res2=r2h)
+        y_mat = T.conv2d(xh, wh, bias=f32(b), res=r1h, res2=up)
+    assert torch.equal(y, y_mat)
+    assert rel(y, ref.permute(0, 2, 3, 1)) < 2e-3
+    if H * W >= 64 * 64:  # the product routes it the same way
+        assert torch.equal(ops.conv2d(xh, wh, bias=f32(b), res=r1h, res2=r2h), y)
+    with T.route(hconv=0, force_tile=-2):  # no upsampling epilogue on this route: rejected by the C ABI
+        assert T.lib.vda_conv2d_res2_upsample_ok(BT, H, W, Cin, 256, 3, 1, 1) == 0
+        with pytest.raises(RuntimeError, match="upsampled res2"):
+            T.conv2d(xh, wh, bias=f32(b), res=r1h, res2=r2h)
+
+
+def test_conv_res2_upsample_op_fallback():
+    """The torch op materialises a lower-resolution res2 when the conv route has no upsampling
+    epilogue (a 37^2 map: the implicit-GEMM / strip routes): same bits as the explicit upsample."""
+    BT, Cin, H, W = 2, 256, 37, 37
+    x, w = rnd(BT, Cin, H, W, seed=310), rnd(256, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=311)
+    r2 = rnd(BT, 256, 19, 19, seed=312)
+    nh = lambda t: h(t.permute(0, 2, 3, 1).contiguous())
+    xh, wh, r2h = nh(x), nh(w), nh(r2)
+    y = ops.conv2d(xh, wh, res2=r2h)
+    assert torch.equal(y, ops.conv2d(xh, wh, res2=ops.upsample_bilinear(r2h, H, W)))
+
+
 @pytest.mark.parametrize("M,N,K", [(4001, 1024, 1024), (43840, 1024, 4096), (4001, 384, 1536), (5003, 768, 768),
                                    (300, 1024, 256), (4001, 1024, 512)])
 def test_gemm_epilogue_row_stats(M, N, K):

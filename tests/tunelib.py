@@ -66,6 +66,8 @@ class TuneLib:
             e.res, e.ldres = res.data_ptr(), Cout
         if res2 is not None:
             e.res2, e.ldres2 = res2.data_ptr(), Cout
+            if tuple(res2.shape[1:3]) != (Ho, Wo):  # read through the upsample in the epilogue
+                e.res2_h, e.res2_w = res2.shape[1], res2.shape[2]
         wsb = self.lib.vda_conv2d_workspace(BT, H, W, Cin, Cout, ks, stride, pad)
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=x.device)
         st = torch.cuda.current_stream().cuda_stream

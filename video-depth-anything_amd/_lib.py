@@ -21,6 +21,7 @@ if os.environ.get("VDA_LIB_OVERRIDE"):  # tuning builds: the op library linked n
 # Every symbol include/vda.h declares (checked by tests/test_capi.py).
 EXPORTED = (
     "vda_version", "vda_epilogue_size", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
+    "vda_conv2d_res2_upsample_ok",
     "vda_row_stats", "vda_groupnorm", "vda_groupnorm_workspace",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
@@ -52,7 +53,7 @@ class Epilogue(ctypes.Structure):
         ("ldres2", c_int64), ("act", c_int32), ("store", c_int32), ("ps_k", c_int32),
         ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
         ("ln_stats", c_void_p), ("ln_colsum", c_void_p), ("ln_parts", c_int32), ("ln_eps", c_float),
-        ("stats_out", c_void_p),
+        ("stats_out", c_void_p), ("res2_h", c_int32), ("res2_w", c_int32),
     ]
 
 
@@ -70,6 +71,7 @@ def _declare(lib):
         "vda_gemm": ([P, L, P, P, L, I, I, I, EP, P], I),
         "vda_conv2d": ([P, P, P, I, I, I, I, I, I, I, I, I, I, I, EP, P, L, P], I),
         "vda_conv2d_workspace": ([I, I, I, I, I, I, I, I], L),
+        "vda_conv2d_res2_upsample_ok": ([I, I, I, I, I, I, I, I], I),
         "vda_layernorm": ([P, L, P, P, P, I, I, F, I, P], I),
         "vda_row_stats": ([P, L, P, I, I, F, P], I),
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),

@@ -228,12 +228,6 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 constexpr int SA_KT = 64;    // keys per tile
 constexpr int SA_QB = 128;   // queries per block
 constexpr int SA_NBUF = 3;   // K/V ring depth
-#ifndef VDA_SA_PRIO
-#define VDA_SA_PRIO 0
-#endif
-#ifndef VDA_SA_ABL
-#define VDA_SA_ABL 0
-#endif
 
 __device__ __forceinline__ int sa_kslot(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 __device__ __forceinline__ int sa_vslot(int row, int c) { return row * 8 + (c ^ (((row >> 1) & 1) << 2)); }
@@ -334,15 +328,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
             if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) sc[kb][r] = -INFINITY;
       }
     };
-#if VDA_SA_PRIO & 1
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
     qk();
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-#else
-    qk();
-#endif
     auto tile_max = [&]() {
       float mx = fmaxf(fmaxf(sc[0][0], sc[0][1]), sc[0][2]);
 #pragma unroll
@@ -369,11 +355,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-#if VDA_SA_ABL == 1  // timing-only: a plain multiply instead of the transcendental
-          const float pv = sc[kb][r] * 0x1p-12f;
-#else
           const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
-#endif
           if (kb == 0) t0 += pv;
           else t1 += pv;
           pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
@@ -396,10 +378,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
       }
     }
     lsum += t0 + t1;
-#if VDA_SA_PRIO & 2
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
     for (int ps = 0; ps < 4; ++ps) {  // the two output tiles' chains interleaved
 #pragma unroll
@@ -411,18 +389,12 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
         o[dt] = mfma32(vf, pf[ps], o[dt]);
       }
     }
-#if VDA_SA_PRIO & 2
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   };
   const int ntiles = (N + SA_KT - 1) / SA_KT;
   auto enter = [&](int kt) {  // tile kt landed and visible; ring slot of kt-1 free -> prefetch kt+2
     if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if VDA_SA_ABL != 3  // timing-only: no barrier (races)
     __builtin_amdgcn_s_barrier();
-#endif
     if (kt + 2 < ntiles) dma(kt + 2);
   };
   dma(0);
@@ -453,227 +425,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
         for (int r = 0; r < 4; ++r) v[r] = (h16)(o[dt][gq * 4 + r] * inv);
         *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
       }
-  }
-}
-
-// =============================================================================================
-// Spatial attention v3, D = 64: a wave owns 64 queries, two 32-query column blocks u = 0, 1 of the
-// v2 layout above.  Every K fragment (ds_read_b128) and transposed V read feeds two MFMAs instead
-// of one, and a tile carries two independent QK -> softmax -> PV chains, ordered so that block 0's
-// softmax VALU sits between block 1's QK MFMAs and block 1's between block 0's PV MFMAs.  Block =
-// 4 waves x 64 queries; waves whose queries all lie past N only stage K / V.  Ring, DMA, swizzles,
-// deferred re-base and the XCD map as in v2.
-// =============================================================================================
-constexpr int SA64_QB = 256;  // queries per block
-#ifndef VDA_SA64
-#define VDA_SA64 0
-#endif
-__global__ __launch_bounds__(256, 2) void spatial_attn64_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                                int N, int H, int nqb, int nblocks, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) h16 sKV[SA_NBUF][2][SA_KT * SD];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int id = blockIdx.x;
-  const int per = nblocks >> 3;
-  if (id < per * 8) id = (id & 7) * per + (id >> 3);
-  const int qb = __builtin_amdgcn_readfirstlane(id % nqb), bh = id / nqb;
-  const int h = __builtin_amdgcn_readfirstlane(bh % H), b = __builtin_amdgcn_readfirstlane(bh / H);
-  const int C = H * SD;
-  const long ld = 3L * C;
-  const h16* base = qkv + (long)b * N * ld + h * SD;
-  const int r32 = lane & 31, hf = lane >> 5;
-  const int qw = __builtin_amdgcn_readfirstlane(qb * SA64_QB + wave * 64);  // the wave's first query
-  const bool active = qw < N;
-
-  h8 qf[2][4];
-#pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int q = qw + u * 32 + r32;
-      h8 t = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (q < N) t = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + ks * 16 + hf * 8));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] = (h16)((float)t[e] * scale_log2);
-      qf[u][ks] = t;
-    }
-
-  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
-  unsigned voff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
-    const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
-    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
-    voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
-  }
-  auto dma = [&](int kt) {
-    const int buf = kt % SA_NBUF;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
-                                               (int)(kt * SA_KT * ld * 2), 0, 0);
-    }
-  };
-
-  f16x o[2][2] = {{f16x{}, f16x{}}, {f16x{}, f16x{}}};
-  f16x negm[2] = {f16x{}, f16x{}};
-  float mrun[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
-  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  unsigned kofs[4], vofs[2];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kofs[ks] = (unsigned)sa_kslot(r32, ks * 2 + hf) * 16u;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int col = dt * 32 + (grp & 1) * 16 + 4 * p4, r0 = 4 * (grp >> 1) + q4;
-    vofs[dt] = (unsigned)(sa_vslot(r0, col >> 3) * 8 + (col & 7)) * 2u;
-  }
-
-  auto tile = [&](int kt, auto first_tag, auto mask_tag) {
-    constexpr bool FIRST = decltype(first_tag)::value;
-    constexpr bool MASK = decltype(mask_tag)::value;
-    unsigned bo;
-    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % SA_NBUF), "n"(2 * SA_KT * SD * 2));
-    const char* kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
-    const char* vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
-    f16x sc[2][2];
-    auto qk = [&](int u) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
-          sc[u][kb] = mfma32(kf, qf[u][ks], ks == 0 ? negm[u] : sc[u][kb]);
-        }
-      if constexpr (MASK) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) sc[u][kb][r] = -INFINITY;
-      }
-    };
-    auto tile_max = [&](int u) {
-      float mx = fmaxf(fmaxf(sc[u][0][0], sc[u][0][1]), sc[u][0][2]);
-#pragma unroll
-      for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[u][0][r]), sc[u][0][r + 1]);
-      mx = fmaxf(fmaxf(mx, sc[u][0][15]), sc[u][1][0]);
-#pragma unroll
-      for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[u][1][r]), sc[u][1][r + 1]);
-      mx = fmaxf(mx, sc[u][1][15]);
-      return half_max(mx);
-    };
-    auto rebase = [&](int u, float sh) {
-      mrun[u] += sh;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) negm[u][r] = -mrun[u];
-      sc[u][0] -= sh;
-      sc[u][1] -= sh;
-    };
-    h8 pf[2][4];
-    float ts[2];
-    auto expo = [&](int u) {
-      float t0 = 0.f, t1 = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sc[u][kb][r]);
-          if (kb == 0) t0 += pv;
-          else t1 += pv;
-          pf[u][kb * 2 + (r >> 3)][r & 7] = (h16)pv;
-        }
-      ts[u] = t0 + t1;
-    };
-    auto check = [&](int u) {  // rare: re-base on the true tile max and redo block u's tile
-      if (__any(!(ts[u] <= 32768.f))) {
-        qk(u);
-        const float sh = fmaxf(tile_max(u), 0.f);
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-        lsum[u] *= alpha;
-        o[u][0] *= alpha;
-        o[u][1] *= alpha;
-        rebase(u, sh);
-        expo(u);
-      }
-    };
-    auto pv = [&](int u) {
-#pragma unroll
-      for (int ps = 0; ps < 4; ++ps)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const char* va = vbase + vofs[dt] + ps * 2048;
-          const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
-          const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
-          const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-          o[u][dt] = mfma32(vf, pf[u][ps], o[u][dt]);
-        }
-    };
-    if constexpr (FIRST) {
-      qk(0);
-      qk(1);
-      rebase(0, tile_max(0));
-      rebase(1, tile_max(1));
-      expo(0);
-      expo(1);
-      pv(0);
-      pv(1);
-    } else {
-      qk(0);
-      qk(1);
-      expo(0);  // beside block 1's QK MFMAs
-      check(0);
-      pv(0);
-      expo(1);  // beside block 0's PV MFMAs
-      check(1);
-      pv(1);
-    }
-    lsum[0] += ts[0];
-    lsum[1] += ts[1];
-  };
-  const int ntiles = (N + SA_KT - 1) / SA_KT;
-  auto enter = [&](int kt) {
-    if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < ntiles) dma(kt + 2);
-  };
-  dma(0);
-  if (ntiles > 1) dma(1);
-  const bool tail = N % SA_KT != 0;
-  const int nfull = ntiles - (tail ? 1 : 0);
-  if (!active) {  // no query of this wave is real: stage the wave's share of K / V only
-    for (int kt = 0; kt < ntiles; ++kt) enter(kt);
-    return;
-  }
-  enter(0);
-  if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{});
-  else tile(0, std::true_type{}, std::false_type{});
-  for (int kt = 1; kt < nfull; ++kt) {
-    enter(kt);
-    tile(kt, std::false_type{}, std::false_type{});
-  }
-  if (tail && ntiles > 1) {
-    enter(ntiles - 1);
-    tile(ntiles - 1, std::false_type{}, std::true_type{});
-  }
-#pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const float inv = 1.f / half_sum(lsum[u]);
-    const int q = qw + u * 32 + r32;
-    if (q < N) {
-      h16* op = out + ((long)b * N + q) * C + h * SD;
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
-          h4 v;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (h16)(o[u][dt][gq * 4 + r] * inv);
-          *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
-        }
-    }
   }
 }
 
@@ -949,12 +700,6 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
     dim3 grid((N + SQB - 1) / SQB, H, B);
     hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, scale * 1.4426950408889634f);
-  } else if (VDA_SA64) {
-    const int nqb = (N + SA64_QB - 1) / SA64_QB;
-    const long nb = (long)nqb * H * B;
-    VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
-    hipLaunchKernelGGL(spatial_attn64_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
-                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
   } else {
     const int nqb = (N + SA_QB - 1) / SA_QB;
     const long nb = (long)nqb * H * B;

@@ -523,6 +523,7 @@ extern "C" int vda_gemm_f32(const float* x, int64_t ldx, const float* w, float* 
   VDA_CHECK_ARG(!epi->rowbias || (epi->rdiv > 0 && epi->rmod > 0), "rowbias needs rdiv, rmod > 0");
   VDA_CHECK_ARG(!epi->ln_stats, "fp32 GEMM: no LayerNorm fold (the fp32 mode runs vda_layernorm_f32)");
   VDA_CHECK_ARG(!epi->stats_out, "fp32 GEMM: no row statistics output");
+  VDA_CHECK_ARG(epi->res2_h == 0 && epi->res2_w == 0, "fp32 GEMM: no upsampled res2");
   F32Params p{};
   p.x = x; p.ldx = ldx; p.w = w; p.y = y; p.ldy = ldy; p.M = M; p.N = N; p.K = K; p.epi = *epi;
   return launch_f32<false>(p, (hipStream_t)stream);
@@ -535,6 +536,7 @@ extern "C" int vda_conv2d_f32(const float* x, const float* w, float* y, int32_t 
   VDA_CHECK_ARG(BT > 0 && H > 0 && W > 0 && ks > 0 && stride > 0 && pad >= 0, "bad conv geometry");
   VDA_CHECK_ARG(Cin % 4 == 0 && Cout % 4 == 0, "fp32 conv needs Cin, Cout multiples of 4");
   VDA_CHECK_ARG(epi->act != VDA_ACT_GEGLU && epi->store == VDA_STORE_ROWS, "conv epilogue: no GEGLU / pixel shuffle");
+  VDA_CHECK_ARG(epi->res2_h == 0 && epi->res2_w == 0, "fp32 conv: no upsampled res2 (materialise it)");
   F32Params p{};
   p.x = x; p.w = w; p.y = y; p.ldy = Cout;
   p.H = H; p.W = W; p.Cin = Cin; p.ks = ks; p.stride = stride; p.pad = pad; p.pre_relu = pre_relu;

@@ -63,7 +63,8 @@ int vda_row_partials_launch(const void* y, int64_t ldy, float* out, int32_t rows
 // halo-tiled phased 3x3 conv, Cout = 256 (vda_hconv.hip)
 bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout);
 int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
-                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st);
+                   const void* res, const void* res2, int res2_h, int res2_w, int BT, int H, int W, int Cin, int Cout,
+                   hipStream_t st);
 
 namespace {
 
@@ -1820,6 +1821,7 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   p.epi = epi ? *epi : default_epi();
   if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
+  VDA_CHECK_ARG(p.epi.res2_h == 0 && p.epi.res2_w == 0, "upsampled res2: vda_conv2d only");
   int rc = check_epi(p.epi, N);
   if (rc) return rc;
   if (p.epi.ln_stats && p.epi.rowbias) {  // only the phased 256x256 route (EK 3) implements the pair
@@ -1842,12 +1844,23 @@ static bool conv_takes_strip(int BT, int H, int W, int Cin, int Cout, int ks, in
   return g_force_tile == -3 || (g_force_tile == -1 && (Cin >= 512 || strip_tiles * 2 <= cu_count()));
 }
 
+// the halo-tiled 256-channel conv route (the only one whose epilogue reads an upsampled res2)
+static bool conv_takes_hconv(int BT, int H, int W, int Cin, int Cout, int ks, int stride, int pad) {
+  return ks == 3 && stride == 1 && pad == 1 && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout);
+}
+
 extern "C" int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
                                         int32_t stride, int32_t pad) {
   if (BT <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
-  if (ks == 3 && stride == 1 && pad == 1 && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout)) return 0;
+  if (conv_takes_hconv(BT, H, W, Cin, Cout, ks, stride, pad)) return 0;
   if (!conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0)) return 0;
   return vda_conv_strip_ws_bytes(BT, H, W, Cin, Cout);
+}
+
+extern "C" int vda_conv2d_res2_upsample_ok(int32_t BT, int32_t H, int32_t W, int32_t Cin, int32_t Cout, int32_t ks,
+                                           int32_t stride, int32_t pad) {
+  if (BT <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
+  return conv_takes_hconv(BT, H, W, Cin, Cout, ks, stride, pad) ? 1 : 0;
 }
 
 extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int32_t H, int32_t W,
@@ -1876,6 +1889,18 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   VDA_CHECK_ARG(!p.epi.stats_out && !p.epi.ln_stats, "conv: no LayerNorm fold / row statistics");
   int rc = check_epi(p.epi, Cout);
   if (rc) return rc;
+  const bool res2_up = p.epi.res2_h > 0 || p.epi.res2_w > 0;
+  if (res2_up) {  // refinenet1's skip add on the previous block's output, upsampled in the epilogue
+    VDA_CHECK_ARG(p.epi.res2 && p.epi.res2_h > 0 && p.epi.res2_w > 0 && p.epi.ldres2 == Cout && p.up_h == 0 &&
+                      !p.epi.gamma && !p.epi.rowbias && (!p.epi.res || p.epi.ldres == Cout) &&
+                      p.epi.res2_h <= p.Ho && p.epi.res2_w <= p.Wo &&
+                      (long)p.epi.res2_h * p.epi.res2_w * Cout * 2 < (1L << 31) &&
+                      conv_takes_hconv(BT, H, W, Cin, Cout, ks, stride, pad),
+                  "upsampled res2 needs the halo conv route (vda_conv2d_res2_upsample_ok), a [BT, h <= Ho, w <= Wo, "
+                  "Cout] source, no gamma / rowbias / input upsample");
+    return vda_conv_hconv(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2,
+                          p.epi.res2_h, p.epi.res2_w, BT, H, W, Cin, Cout, (hipStream_t)stream);
+  }
   if (p.up_h > 0) {
     // 3x3 conv on a bilinear resize with 128 outputs (output_conv1 on refinenet1's x2 resize): the
     // halo conv with the resize fused into its patch staging (bit-identical to resize + conv)
@@ -1889,10 +1914,10 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   }
   // large maps with 256 output channels (the refinenet RCU convs and layer1_rn at 148^2): the
   // halo-tiled phased conv stages each input patch once per 64-channel slab instead of 9 times
-  if (ks == 3 && stride == 1 && pad == 1 && !p.epi.gamma && !p.epi.rowbias && (!p.epi.res || p.epi.ldres == Cout) &&
-      (!p.epi.res2 || p.epi.ldres2 == Cout) && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout)) {
-    rc = vda_conv_hconv(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, BT, H, W,
-                        Cin, Cout, (hipStream_t)stream);
+  if (!p.epi.gamma && !p.epi.rowbias && (!p.epi.res || p.epi.ldres == Cout) && (!p.epi.res2 || p.epi.ldres2 == Cout) &&
+      conv_takes_hconv(BT, H, W, Cin, Cout, ks, stride, pad)) {
+    rc = vda_conv_hconv(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, pre_relu, p.epi.res, p.epi.res2, 0, 0, BT, H,
+                        W, Cin, Cout, (hipStream_t)stream);
     if (rc != 1) return rc;
   }
   if (conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0) && !p.epi.gamma && !p.epi.rowbias &&

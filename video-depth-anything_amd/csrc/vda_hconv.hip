@@ -2,7 +2,10 @@
 //
 // Serves the FeatureFusionBlock RCU convs and layerN_rn convs at the large decoder maps
 // (util/blocks.py:68-91 ResidualConvUnit, dpt.py:100-104 scratch.layerN_rn; 148^2 and 74^2 for a
-// 518^2 input): y = act(conv3x3(pre_relu ? relu(x) : x) + bias) + res + res2, NHWC fp16.
+// 518^2 input): y = act(conv3x3(pre_relu ? relu(x) : x) + bias) + res + res2, NHWC fp16.  res2 may be
+// a half-resolution map read through the bilinear (align_corners=True) upsample in the epilogue
+// (refinenet1's skip input, blocks.py:146-158): 4 source pixels per output pixel, interpolated with
+// the same float ops as vda_upsample_bilinear, so the upsampled map is never written.
 //
 // The implicit-GEMM conv (vda_gemm.hip) re-gathers every input pixel once per tap: its 256-pixel
 // X tile is refetched 9 times per 64-channel slab, and with Cout = 256 there is a single N tile, so
@@ -55,7 +58,8 @@ struct HconvArgs {
   h16* y;           // [BT, H, W, 256]
   const float* bias;
   const h16* res;   // [BT, H, W, 256] or null
-  const h16* res2;
+  const h16* res2;  // [BT, H, W, 256], or [BT, r2h, r2w, 256] read through the bilinear upsample
+  int r2h, r2w;     // > 0: res2 is upsampled (align_corners=True) to the output grid in the epilogue
   int H, W, Cin, relu_out;
   int tiles_x, tiles_y, ntiles;
 };
@@ -294,10 +298,39 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     const int yy = y0 + (it >> 1), xx = x0 + row0 + 16 * (it & 1);
     return (yy < H && xx < W) ? (unsigned)(((yy * W + xx) * 256 + q * 8) * 2) : 0x80000000u;
   };
-  const int nres = (a.res ? 1 : 0) + (a.res2 ? 1 : 0);
-  const h16* r1p = a.res ? a.res : a.res2;
+  const bool up2 = a.r2h > 0;
+  const h16* pres2 = up2 ? nullptr : a.res2;  // a same-grid res2
+  const int nres = (a.res ? 1 : 0) + (pres2 ? 1 : 0);
+  const h16* r1p = a.res ? a.res : pres2;
   const __amdgpu_buffer_rsrc_t rr1 = rsrc(r1p ? r1p : a.y);
-  const __amdgpu_buffer_rsrc_t rr2 = rsrc(a.res2 ? a.res2 : a.y);
+  const __amdgpu_buffer_rsrc_t rr2 = rsrc(pres2 ? pres2 : a.y);
+  // upsampled res2: the 4 source pixels of output pixel `it` (clamped into the map: rows past H / W
+  // are never stored) and its weights, as vda_upsample_bilinear forms them
+  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((up2 ? a.res2 : a.y) + (up2 ? (long)bt * a.r2h * a.r2w * 256 : fbase)), (short)0,
+      up2 ? (int)((long)a.r2h * a.r2w * 512) : (int)fbytes, 0x00020000);
+  const float usy = a.r2h > 0 && H > 1 ? (float)(a.r2h - 1) / (float)(H - 1) : 0.f;
+  const float usx = a.r2w > 0 && W > 1 ? (float)(a.r2w - 1) / (float)(W - 1) : 0.f;
+  auto up_load = [&](int it, h8* t4, float& wx, float& wy) {
+    const int yy = min(y0 + (it >> 1), H - 1), xx = min(x0 + row0 + 16 * (it & 1), W - 1);
+    const float fy = usy * (float)yy, fx = usx * (float)xx;
+    const int sy0 = (int)fy, sx0 = (int)fx;
+    const int sy1 = min(sy0 + 1, a.r2h - 1), sx1 = min(sx0 + 1, a.r2w - 1);
+    wy = fy - (float)sy0;
+    wx = fx - (float)sx0;
+    const unsigned r0 = (unsigned)(sy0 * a.r2w), r1 = (unsigned)(sy1 * a.r2w), c8 = (unsigned)q * 16u;
+    t4[0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx0) * 512u + c8, 0, 0));
+    t4[1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx1) * 512u + c8, 0, 0));
+    t4[2] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r1 + sx0) * 512u + c8, 0, 0));
+    t4[3] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r1 + sx1) * 512u + c8, 0, 0));
+  };
+  constexpr int UPD = 2;  // upsampled-res2 prefetch depth (pixels)
+  h8 u4[UPD][4];
+  float uwx[UPD], uwy[UPD];
+  if (up2) {
+#pragma unroll
+    for (int it = 0; it < UPD; ++it) up_load(it, u4[it], uwx[it], uwy[it]);
+  }
   constexpr int PD = 4;
   h8 q1[PD], q2[PD];
   if (nres >= 1) {
@@ -322,6 +355,11 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
       t += q2[it % PD];
       if (it + PD < 16) q2[it % PD] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, voff(it + PD), 0, 0));
     }
+    if (up2) {
+      const int sl = it % UPD;
+      t += bilerp8(u4[sl][0], u4[sl][1], u4[sl][2], u4[sl][3], uwx[sl], uwy[sl]);
+      if (it + UPD < 16) up_load(it + UPD, u4[sl], uwx[sl], uwy[sl]);
+    }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vo, 0, 2);
   }
 }
@@ -343,11 +381,14 @@ bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout) {
 }
 
 int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
-                   const void* res, const void* res2, int BT, int H, int W, int Cin, int Cout, hipStream_t st) {
+                   const void* res, const void* res2, int res2_h, int res2_w, int BT, int H, int W, int Cin, int Cout,
+                   hipStream_t st) {
   if (!vda_conv_hconv_serves(BT, H, W, Cin, Cout)) return 1;
   HconvArgs a{};
   a.x = (const h16*)x; a.w = (const h16*)w; a.y = (h16*)y; a.bias = bias;
   a.res = (const h16*)res; a.res2 = (const h16*)res2;
+  a.r2h = res2 && res2_h > 0 && res2_w > 0 ? res2_h : 0;
+  a.r2w = a.r2h > 0 ? res2_w : 0;
   a.H = H; a.W = W; a.Cin = Cin; a.relu_out = relu_out;
   a.tiles_x = (W + HC_TC - 1) / HC_TC;
   a.tiles_y = (H + HC_TR - 1) / HC_TR;

@@ -192,6 +192,7 @@ Tensor conv_transpose_ks(const Tensor& x, const Tensor& w, const Tensor& bias, i
 }
 
 // ---- NHWC conv ---------------------------------------------------------------------------------
+Tensor upsample_bilinear(const Tensor& x, int64_t Ho, int64_t Wo);
 Tensor conv2d(const Tensor& x, const Tensor& w, int64_t ks, int64_t stride, int64_t pad, OptT bias, bool pre_relu,
               int64_t act, OptT res, OptT res2, at::OptionalIntArrayRef up) {
   const auto dt = act_dtype(x);
@@ -213,8 +214,27 @@ Tensor conv2d(const Tensor& x, const Tensor& w, int64_t ks, int64_t stride, int6
   const at::OptionalDeviceGuard g(x.device());
   optional<Tensor> r, r2;
   if (res) r = res->reshape({-1, Cout});
-  if (res2) r2 = res2->reshape({-1, Cout});
+  int32_t r2h = 0, r2w = 0;
+  if (res2) {
+    Tensor s2 = *res2;
+    if (s2.dim() == 4 && (s2.size(1) != Ho || s2.size(2) != Wo)) {
+      // a lower-resolution skip input (the previous fusion block's output, blocks.py:156-158): read
+      // through the bilinear upsample in the conv epilogue where the route has it, else materialised
+      TORCH_CHECK(s2.size(0) == BT && s2.size(3) == Cout && s2.size(1) <= Ho && s2.size(2) <= Wo && s2.is_contiguous(),
+                  "vda conv2d: a res2 of another grid must be a contiguous [BT, h <= Ho, w <= Wo, Cout] map, got ",
+                  s2.sizes());
+      if (dt != at::kFloat && uh == 0 && vda_conv2d_res2_upsample_ok(BT, H, W, Cin, Cout, ks, stride, pad)) {
+        r2h = (int32_t)s2.size(1);
+        r2w = (int32_t)s2.size(2);
+      } else {
+        s2 = upsample_bilinear(s2, Ho, Wo);
+      }
+    }
+    r2 = s2.reshape({-1, Cout});
+  }
   vda_epilogue e = make_epi(x, bias, c10::nullopt, 1, 1, c10::nullopt, r, r2, act, dt);
+  e.res2_h = r2h;
+  e.res2_w = r2w;
   int rc;
   if (dt == at::kFloat) {
     TORCH_CHECK(uh == 0, "vda conv2d: the fused-upsample loader is fp16-only");

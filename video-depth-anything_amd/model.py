@@ -614,8 +614,10 @@ class VideoDepthAnything(nn.Module):
         if sel is not None:
             p3 = p3.index_select(0, torch.tensor(sel, dtype=torch.long, device=p3.device))
         y, _ = self._fusion(P.ref[2], p3, r2, None)
-        p2 = ops.upsample_bilinear(y, r1.shape[1], r1.shape[2])
-        y, _ = self._fusion(P.ref[1], p2, r1, None)  # refinenet1: scale_factor 2
+        # refinenet2's upsample to r1's grid (blocks.py:156-158) is only refinenet1's skip input (res2 of
+        # its RCU conv2, blocks.py:146-150): the conv reads it through the upsample in its epilogue
+        # (bit-identical; materialised by the op where the conv route has no such epilogue)
+        y, _ = self._fusion(P.ref[1], y, r1, None)  # refinenet1: scale_factor 2
         H1, W1 = 2 * y.shape[1], 2 * y.shape[2]
         # refinenet1's x2 bilinear upsample (blocks.py:151-158) fused into output_conv1's patch staging
         # (fp16: the halo conv builds each patch by interpolation; fp32 mode materialises the resize)
