@@ -2,7 +2,7 @@
 us per call, TFLOP/s (4·B·H·N²·D), and rel error vs torch SDPA on the same fp16 inputs.  With VDA_LIB_OVERRIDE=build/tune/libvda.so and
 VDA_ATTN_OLD=1 the round-1 kernel (vda_debug_attn)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 import torch.nn.functional as F
 from vda_amd import ops, _lib

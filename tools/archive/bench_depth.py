@@ -1,6 +1,6 @@
 """Depth-head tail microbenchmark (ViT-L 32x518^2 shapes), per kernel config."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 L = _lib.lib()

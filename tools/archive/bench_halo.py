@@ -1,7 +1,7 @@
 """Halo-kernel microbenchmark: output_conv1 (conv3x3 256->128 at 32x296^2) and the depth tail
 (resize to 518^2 + halo conv), each vs its implicit-GEMM fallback.  us per call, same process."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 L = _lib.lib()

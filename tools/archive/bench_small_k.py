@@ -3,7 +3,7 @@ the tuning build's vda_debug_force_tile (tuning tool).  usage: python tools/benc
 Prints us per call per configuration (-1 = the automatic choice) and checks every configuration's
 output against the automatic one (rel-L1)."""
 import ctypes, os, statistics, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import _lib
 L = ctypes.CDLL(_lib.TUNE_LIB_PATH); _lib._declare(L)

@@ -2,7 +2,7 @@
 forward_single_image step on ViT-L at 518x518 with a 31-frame context and alignment rows, and the
 whole driver on a synthetic uint8 video (preprocess + store + alignment included).  Diagnostic."""
 import os, sys, time
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import torch
 import vda_amd

@@ -2,7 +2,7 @@
 RCU convs, 32 frames at 518^2) on the strip-tiled halo kernel vs the implicit GEMM
 (vda_debug_force_tile(-2)).  us per call and TFLOP/s, same process."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 L = _lib.lib()

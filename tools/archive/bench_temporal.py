@@ -1,7 +1,7 @@
 """Temporal attention (motion_module.py:302-322) at the ViT-L 32x518^2 motion-module shapes: us per
 call and HBM GB/s (q, k, v read + o written).  VDA_TA_OLD=1 selects the direct-load kernel (A/B; tuning build: VDA_LIB_OVERRIDE=build/tune/libvda.so)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 if os.environ.get("VDA_TA_OLD"):

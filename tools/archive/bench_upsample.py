@@ -2,7 +2,7 @@
 frames: 148^2 -> 296^2 (256 ch, refinenet1) and 296^2 -> 518^2 (128 ch, output_conv2 input).
 Prints us per call and GB/s of (output + input) bytes."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops
 for (hi, ho, c) in [(148, 296, 256), (296, 518, 128), (74, 148, 256)]:

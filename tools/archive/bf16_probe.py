@@ -1,7 +1,7 @@
 """Power/clock probe: the phased GEMM on fp16 vs bf16-bit-pattern operands (experimental lib built with
 -DVDA_MFMA_BF16 multiplies bf16).  usage: VDA_LIB_OVERRIDE=... python tools/bf16_probe.py [bf16]"""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 L = _lib.lib(); L.vda_debug_force_tile(4)

@@ -1,7 +1,7 @@
 """Isolate the implicit-GEMM conv's K-step cost: the same M x N x K (M = 32*148^2, N = 256, K = 2304)
 as a dense GEMM, a 1x1 conv (gather path, no tap re-reads) and the 3x3 conv (Cin = 256)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 L = _lib.lib()

@@ -1,6 +1,6 @@
 """Fixed (prologue + epilogue) vs per-K-tile cost of the phased GEMM: time M x N x K for K = 64..2048."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops
 from vda_amd._lib import ACT_GELU

@@ -1,6 +1,6 @@
 """Persistent-grid / start-stagger probe for the phased GEMM (qkv and fc1 shapes)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from vda_amd import ops, _lib
 from vda_amd._lib import ACT_GELU

@@ -16,7 +16,6 @@ accumulation, statistics and depth tail (dpt_temporal.py:95-97 keeps output_conv
 from __future__ import annotations
 
 import math
-import os
 from typing import Dict, List, Optional
 
 import torch
@@ -232,7 +231,15 @@ class _Packed:
 
 
 class VideoDepthAnything(nn.Module):
-    """Reference-compatible constructor (video_depth.py:36-45) and forward (:58-65)."""
+    """Reference-compatible constructor (video_depth.py:36-45) and forward (:58-65).
+
+    Per-instance schedule switches (A/B experiments only; set before the first forward, they are part
+    of the packed-weight cache key): ``fold_layernorms`` folds the encoder's norm1 / norm2 into the
+    qkv / fc1 GEMMs (fp16 mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
+    proj / fc2 epilogues instead of a separate pass.  No environment variable changes the schedule."""
+
+    fold_layernorms: bool = True
+    epilogue_stats: bool = True
 
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
@@ -270,7 +277,7 @@ class VideoDepthAnything(nn.Module):
     def _pack(self, device, fp32: bool = False) -> _Packed:
         """Kernel-ready weights for ``device``: fp16 (the shipped mode) or, with ``fp32``, fp32 copies
         for the fp32-mode kernels (same layouts, vda.h *_f32)."""
-        key = f"{device}|{'f32' if fp32 else 'f16'}"
+        key = f"{device}|{'f32' if fp32 else 'f16'}|{int(bool(self.fold_layernorms))}"
         if key in self._packed:
             return self._packed[key]
         dev = torch.device(device)
@@ -294,7 +301,7 @@ class VideoDepthAnything(nn.Module):
         # b' = W beta + b, colsum = sum_k W' (of the fp16 W' the kernel multiplies); the GEMM epilogue
         # applies rstd * (x W'^T - mean colsum) + b' from per-row statistics (vda_row_stats), so the
         # normalised copy of the token tensor is never written or re-read.
-        P.lnfold = not fp32 and os.environ.get("VDA_NO_LNFOLD", "0") != "1"
+        P.lnfold = not fp32 and bool(self.fold_layernorms)
 
         def _ln_fold(lin, ln):
             w = lin.weight.detach().float()
@@ -525,7 +532,7 @@ class VideoDepthAnything(nn.Module):
         # update the residual stream (stats_out), so no LayerNorm reads the 90-MB token matrix again
         C = P.C
         nparts = (C + 255) // 256
-        epistats = P.lnfold and nparts <= 4 and os.environ.get("VDA_NO_EPISTATS", "0") != "1"
+        epistats = P.lnfold and nparts <= 4 and bool(self.epilogue_stats)
         if epistats:
             # one spare row: the LN-folded GEMMs stage the partials in 16-byte pieces (vda.h ln_parts)
             st_a = torch.empty(tok.shape[0] + 1, nparts, 2, device=tok.device, dtype=torch.float32)
