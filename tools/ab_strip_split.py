@@ -1,8 +1,8 @@
 """Strip-conv split count A/B through the tuning build (tuning tool, not product code).
 
 usage: python tools/ab_strip_split.py [--rounds R]
-The 37^2 / 19^2 3x3 convs with 256 outputs (layer3_rn, layer4_rn: Cin 1024; RCU at 19^2: Cin 256) of a
-32-frame clip, timed with every split count the kernel accepts (vda_debug_strip_split) against the
+The 37^2 / 19^2 (and 518x924: 37x66 / 19x33) 3x3 convs with 256 outputs (layer3_rn, layer4_rn: Cin 1024;
+RCU at 19^2: Cin 256) of a 32-frame clip, timed with every split count the kernel accepts (vda_debug_strip_split) against the
 automatic choice; outputs compared with the unsplit result (the split sums fp32 partials in another
 order: close, not bit-identical).
 """
@@ -18,8 +18,10 @@ from tunelib import tune_lib
 rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
 T = tune_lib()
 torch.manual_seed(0)
-for name, BT, H, Cin in [("layer3_rn", 32, 37, 1024), ("layer4_rn", 32, 19, 1024), ("rcu19", 32, 19, 256)]:
-    x = (torch.randn(BT, H, H, Cin, device="cuda") * 0.5).half()
+for name, BT, H, W, Cin in [("layer3_rn", 32, 37, 37, 1024), ("layer4_rn", 32, 19, 19, 1024), ("rcu19", 32, 19, 19, 256),
+                            ("layer3_rn_924", 32, 37, 66, 1024), ("layer4_rn_924", 32, 19, 33, 1024),
+                            ("rcu19_924", 32, 19, 33, 256)]:
+    x = (torch.randn(BT, H, W, Cin, device="cuda") * 0.5).half()
     w = (torch.randn(256, 3, 3, Cin, device="cuda") * (9 * Cin) ** -0.5).half()
     res = {}
     for s in (0, 1, 2, 4, 8):
