@@ -111,6 +111,28 @@ def test_epilogue_combinations_rejected():
     assert lib.vda_gemm_f32(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
 
 
+def test_res2_upsample_validation():
+    """An upsampled res2 (vda_epilogue.res2_h/res2_w) is a conv-epilogue option of the halo-tiled
+    256-channel route only: the GEMM, the fp32 conv and other conv routes reject it before any launch,
+    and vda_conv2d_res2_upsample_ok answers which shapes take it (the model's 148^2 refinenet1 conv)."""
+    lib = _lib.lib()
+    fake = ctypes.c_void_p(0x1000)
+    assert lib.vda_conv2d_res2_upsample_ok(32, 148, 148, 256, 256, 3, 1, 1) == 1
+    assert lib.vda_conv2d_res2_upsample_ok(32, 148, 264, 256, 256, 3, 1, 1) == 1   # 518x924 input
+    assert lib.vda_conv2d_res2_upsample_ok(32, 37, 37, 256, 256, 3, 1, 1) == 0     # implicit-GEMM route
+    assert lib.vda_conv2d_res2_upsample_ok(32, 148, 148, 256, 128, 3, 1, 1) == 0   # Cout 128
+    assert lib.vda_conv2d_res2_upsample_ok(32, 148, 148, 256, 256, 3, 2, 1) == 0   # stride 2
+    e = _lib.Epilogue(rdiv=1, rmod=1, res2=0x2000, ldres2=256, res2_h=74, res2_w=74)
+    assert lib.vda_gemm(fake, 64, fake, fake, 256, 4096, 256, 64, e, None) == -22
+    assert b"vda_conv2d only" in lib.vda_last_error()
+    assert lib.vda_conv2d(fake, fake, fake, 32, 37, 37, 256, 256, 3, 1, 1, 0, 0, 0, e, None, 0, None) == -22
+    assert b"upsampled res2" in lib.vda_last_error()
+    e.res2_h = 200  # larger than the output grid
+    assert lib.vda_conv2d(fake, fake, fake, 32, 148, 148, 256, 256, 3, 1, 1, 0, 0, 0, e, None, 0, None) == -22
+    e.res2_h = 74
+    assert lib.vda_conv2d_f32(fake, fake, fake, 32, 148, 148, 256, 256, 3, 1, 1, 0, e, None) == -22
+
+
 def test_conv_and_attention_validation():
     lib = _lib.lib()
     fake = ctypes.c_void_p(0x1000)
