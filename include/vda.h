@@ -63,19 +63,17 @@ typedef struct vda_epilogue {
   /* LayerNorm folded into the GEMM (block.py:84,87 norm1 / norm2 feeding qkv / fc1): X is the raw
    * row stream x, W holds gamma (.) W_ln, bias holds W_ln beta + b, ln_colsum[n] = sum_k W[n, k] (of the
    * fp16 W actually used), and ln_stats[m] = (mean, rstd) of row m from vda_row_stats.  Then
-   * rstd (x W^T - mean colsum) + bias = LN(x) W_ln^T + b exactly in real arithmetic.  ln_stats holds
-   * an even number of rows (M rounded up to 2).  Row store only, no gamma, activation none / gelu.
+   * rstd (x W^T - mean colsum) + bias = LN(x) W_ln^T + b exactly in real arithmetic.  Row store only, no gamma, activation none / gelu.
    * With a rowbias (the motion-module q/k/v: LN(x) + pe[t] then to_q/k/v, motion_module.py:175,256,
    * 263): bias required, no activation / res / res2 / stats_out, rdiv >= 256, N % 256 == 0,
    * M >= 4096, K % 64 == 0, 16-byte aligned x / y rows (the phased route's EK 3 epilogue; -22
    * otherwise). */
-  const float* ln_stats;  /* [round_up(M, 2), 2] or NULL                              */
+  const float* ln_stats;  /* [M, 2] or NULL                                              */
   const float* ln_colsum; /* [N]                                                     */
   /* ln_parts > 0: ln_stats instead holds [M, ln_parts, 2] partial (sum, sum of squares) of row m
    * over ln_parts column blocks (as written through stats_out by the GEMM that produced X); the
    * epilogue forms mean = sum / K, var = max(sumsq / K - mean^2, 0), rstd = 1 / sqrt(var + ln_eps).
-   * ln_parts <= 4.  The partials are staged in 16-byte pieces: the buffer must extend to a multiple
-   * of 4 floats (one spare row when M * ln_parts is odd). */
+   * ln_parts <= 4.  No padding is needed past [M, ln_parts, 2]: the kernels never read beyond it. */
   int32_t ln_parts;
   float ln_eps;
   /* Producer side: write [M, ceil(N / 256), 2] per-row partial (sum, sum of squares) of the fp16

@@ -749,3 +749,54 @@ def test_gemm_epilogue_row_stats(M, N, K):
     torch.cuda.synchronize()
     assert torch.equal(tok2, tok)
     assert torch.allclose(st2[:M], st[:M], rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("M,P,rowbias,nobias", [(4097, 3, False, False), (4097, 1, False, False), (4097, 0, False, False),
+                                                (4097, 3, False, True), (4097, 0, False, True), (4097, 1, True, False),
+                                                (5003, 3, True, False)])
+def test_gemm_layernorm_fold_odd_stats_exact_size(M, P, rowbias, nobias):
+    """VERDICT r3 item 6 / ADVICE r2-r3: the phased LN-folded GEMM stages the statistics in 16-byte
+    pieces; with M * P odd (or M odd for [M, 2] statistics) the last piece holds one valid entry.  The
+    statistics buffer here is EXACTLY [M, P, 2] (no spare row), carved from the END of a larger
+    allocation whose tail is NaN: a read past it would poison the last row.  Through the C ABI, vs
+    torch fp32 LayerNorm -> Linear (+ the per-frame PE row bias on the EK 3 route); without a bias the
+    staged epilogue's reader runs instead of the register epilogue's."""
+    from vda_amd import _lib
+    lib = _lib.lib()
+    K = 256 * max(P, 1)
+    N = 768 if rowbias else 512
+    S, T = 1024, 4
+    g = torch.Generator().manual_seed(M + P)
+    x = (torch.randn(M, K, generator=g) * 2 + torch.randn(M, 1, generator=g)).half().float()
+    gam, bet = 1 + 0.2 * torch.randn(K, generator=g), 0.1 * torch.randn(K, generator=g)
+    w = torch.randn(N, K, generator=g) * K ** -0.5
+    pe = torch.randn(T, K, generator=g) * 0.5
+    ln = F.layer_norm(x, (K,), gam, bet, eps=1e-5)
+    if rowbias:
+        ln = ln + pe[(torch.arange(M) // S) % T]
+    ref = F.linear(ln, w) - (w @ bet if nobias else 0)
+    wg = (w * gam[None, :]).half()
+    if P > 0:
+        xf = x.view(M, P, 256)
+        stats = torch.stack([xf.sum(2), (xf * xf).sum(2)], -1)  # [M, P, 2]
+    else:
+        mean, var = x.mean(1), x.var(1, unbiased=False)
+        stats = torch.stack([mean, (var + 1e-5).rsqrt()], -1)  # [M, 2]
+    n = stats.numel()
+    big = torch.full((n + 64,), float("nan"), device=DEV)
+    st = big[:n]  # exactly [M, P, 2]; NaN right behind it
+    st.copy_(stats.reshape(-1).to(DEV))
+    xd, wd = h(x), wg.to(DEV)
+    y = torch.empty(M, N, dtype=torch.float16, device=DEV)
+    bias, cs = f32(w @ bet), f32(wg.float().sum(1))
+    rb = f32(pe @ w.t())
+    e = Epilogue(bias=0 if nobias else bias.data_ptr(), ln_stats=st.data_ptr(), ln_colsum=cs.data_ptr(), ln_parts=P, ln_eps=1e-5,
+                 rdiv=S if rowbias else 1, rmod=T if rowbias else 1, rowbias=rb.data_ptr() if rowbias else 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    assert lib.vda_gemm(xd.data_ptr(), K, wd.data_ptr(), y.data_ptr(), N, M, N, K, e, stream) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    err = rel(y, ref)
+    err_last = rel(y[-1:], ref[-1:])
+    print(f"LN fold odd stats M={M} P={P} rowbias={rowbias}: rel-L1 {err:.2e}, last row {err_last:.2e}")
+    assert err < 3e-3 and err_last < 5e-3

@@ -269,3 +269,34 @@ def test_video_frames_already_on_device():
     d_host, _ = V.infer_video_depth(fwd, frames, 24, input_size=56, device="cuda")
     d_dev, _ = V.infer_video_depth(fwd, torch.from_numpy(frames).cuda(), 24, input_size=56, device="cuda")
     assert np.array_equal(d_host, d_dev)
+
+
+@pytest.mark.gpu
+def test_multirank_receive_buffers_survive_side_stream_reuse(monkeypatch):
+    """VERDICT r3 item 4 / ADVICE r3: with world > 1 each round's receive buffers come from a side
+    stream, while rank 0's sink copies them to the host on the current stream.  A stand-in gather
+    returns side-stream device buffers and its wait() delays the current stream, so without the
+    record_stream in ``land`` the side stream's next forward (which allocates and scribbles over
+    same-size blocks) overwrites them before the copies run.  streams=2 must equal streams=1."""
+    class _Work:
+        def wait(self):
+            torch.cuda._sleep(20_000_000)  # hold the current stream so the D2H copies queue late
+
+    def fake_gather(buf, rank, world, group):
+        bufs = [(buf * (1.0 + src)).contiguous() for src in range(world)]
+        return bufs, _Work(), buf
+
+    def fwd(x):
+        for _ in range(3):  # same-size scratch written on this stream: reuses freed receive blocks
+            torch.full((x.shape[0], x.shape[1], x.shape[3], x.shape[4]), -7.0, device=x.device)
+        return (x[:, :, 0] * 3.0 + 1.0).contiguous()
+
+    monkeypatch.setattr(V, "_gather_round", fake_gather)
+    frames = np.random.default_rng(11).integers(0, 256, (150, 48, 64, 3), dtype=np.uint8)
+    out = []
+    for streams in (1, 2):
+        d, _ = V.infer_video_depth(fwd, frames, 24, input_size=56, device="cuda", rank=0, world=2,
+                                   streams=streams)
+        torch.cuda.synchronize()
+        out.append(d)
+    assert np.array_equal(out[0], out[1])

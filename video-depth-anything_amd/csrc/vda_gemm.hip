@@ -712,6 +712,12 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   const float* phi_lds = reinterpret_cast<const float*>(smem + 2 * BUF);
   const unsigned phib = phi_base(phi_lds);
   h16* lnst_lds = smem + 2 * BUF + (TAB ? PHI_LDS_HALVES : 0);  // LNF: [256][2] fp32 (mean, rstd)
+  // LNF: tile row whose last statistics entry sits 2 floats further on in LDS (the global array's
+  // final entry when M * P is odd: its piece was read 8 B early, see lnst_dma), or -1
+  auto lnst_shift_row = [&](int m0_) {
+    const int P1 = p.epi.ln_parts > 0 ? p.epi.ln_parts : 1;
+    return ((p.M * P1) & 1) && p.M - 1 - m0_ < 256 ? p.M - 1 - m0_ : -1;
+  };
 
   // lane id rebuilt per tile by a volatile mbcnt (and the wave index passed in an SGPR): every
   // lane-derived address below is recomputed per tile instead of being hoisted out of the persistent
@@ -895,13 +901,18 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     if constexpr (LNF) {
       if (p.epi.ln_parts <= 0) {  // rows m0 .. m0+255 of [M, 2] fp32 (mean, rstd): 2 pieces of 128 rows, waves 0-1
         if (wave < 2) {
-          const int r = m0_ + wave * 128 + lane * 2;  // this lane's 16 B = rows r, r + 1 (M is even or row r+1 unused)
-          const void* src = r < p.M ? (const void*)(p.epi.ln_stats + (long)r * 2) : (const void*)g_zero_page;
+          const int r = m0_ + wave * 128 + lane * 2;  // this lane's 16 B = rows r, r + 1
+          // M odd: the piece of row M - 1 alone is read 8 B early (rows M - 2, M - 1), never past the
+          // [M, 2] buffer; the readers find that row 8 B further on (lnst_ofs)
+          const long f = (long)r * 2 - (r == p.M - 1 ? 2 : 0);
+          const void* src = r < p.M ? (const void*)(p.epi.ln_stats + f) : (const void*)g_zero_page;
           glds16(src, lnst_lds + wave * 512);
         }
       } else if (wave < 2 * p.epi.ln_parts) {  // rows m0 .. m0+255 of [M, P, 2] partial sums: 2P pieces of 1 KiB
         const long f = (long)m0_ * p.epi.ln_parts * 2 + wave * 256 + lane * 4;  // float index of this lane's 16 B
-        const void* src = f < (long)p.M * p.epi.ln_parts * 2 ? (const void*)(p.epi.ln_stats + f) : (const void*)g_zero_page;
+        const long T = (long)p.M * p.epi.ln_parts * 2;
+        // M * P odd: the last piece holds one valid entry; it is read 8 B early instead of 8 B past the end
+        const void* src = f < T ? (const void*)(p.epi.ln_stats + (f + 4 > T ? f - 2 : f)) : (const void*)g_zero_page;
         glds16(src, lnst_lds + wave * 512);
       }
     }
@@ -1041,16 +1052,19 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       const float* st = reinterpret_cast<const float*>(lnst_lds);
       const int P = e.ln_parts;
       const float invK = 1.f / (float)p.K;
+      const int srow = lnst_shift_row(m0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int rl = wm * 128 + j * 16 + mcol;
+        const int sh = rl == srow ? 2 : 0;
         if (P <= 0) {
-          mr[j] = *reinterpret_cast<const float2*>(st + 2 * rl);
+          mr[j] = *reinterpret_cast<const float2*>(st + 2 * rl + sh);
         } else {
           float sm = 0.f, sq = 0.f;
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + (t < P ? t : 0)));
+            const int tt = t < P ? t : 0;
+            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + tt) + (tt == P - 1 ? sh : 0));
             sm += t < P ? pq.x : 0.f;
             sq += t < P ? pq.y : 0.f;
           }
@@ -1260,16 +1274,18 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       const f4* bv = pbv;  // zero when there is no bias
       const int P = e.ln_parts;
       const float invK = 1.f / (float)p.K;
+      const int srow = lnst_shift_row(m0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int rl = wm * 128 + j * 16 + mcol;
+        const int sh = rl == srow ? 2 : 0;
         float2 mr;
         if (P <= 0) {
-          mr = *reinterpret_cast<const float2*>(st + 2 * rl);
+          mr = *reinterpret_cast<const float2*>(st + 2 * rl + sh);
         } else {  // partial (sum, sumsq) of P column blocks -> (mean, rstd)
           float sm = 0.f, sq = 0.f;
           for (int t = 0; t < P; ++t) {
-            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + t));
+            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + t) + (t == P - 1 ? sh : 0));
             sm += pq.x;
             sq += pq.y;
           }

@@ -91,16 +91,12 @@ vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, in
     need_contig(*ln_stats, at::kFloat, "ln_stats", x);
     need_contig(*ln_colsum, at::kFloat, "ln_colsum", x);
     if (ln_parts > 0) {
-      // the kernels stage the partials in whole 16-byte pieces: the buffer must reach the next multiple
-      // of 4 floats past the last row (allocate M + 1 rows when M * P is odd)
       TORCH_CHECK(ln_parts <= 4 && ln_stats->dim() == 3 && ln_stats->size(0) >= x.size(0) &&
-                      ln_stats->size(1) == ln_parts && ln_stats->size(2) == 2 &&
-                      ln_stats->numel() >= (x.size(0) * ln_parts * 2 + 3) / 4 * 4,
-                  "vda gemm: with ln_parts = P, ln_stats must be [M, P, 2] partial sums (a GEMM's stats_out), P <= 4, "
-                  "padded to a multiple of 4 floats");
+                      ln_stats->size(1) == ln_parts && ln_stats->size(2) == 2,
+                  "vda gemm: with ln_parts = P, ln_stats must be [M, P, 2] partial sums (a GEMM's stats_out), P <= 4");
     } else {
-      TORCH_CHECK(ln_stats->dim() == 2 && ln_stats->size(1) == 2 && ln_stats->size(0) >= (x.size(0) + 1) / 2 * 2,
-                  "vda gemm: ln_stats must be [round_up(M, 2), 2] (from vda.row_stats)");
+      TORCH_CHECK(ln_stats->dim() == 2 && ln_stats->size(1) == 2 && ln_stats->size(0) >= x.size(0),
+                  "vda gemm: ln_stats must be [M, 2] (from vda.row_stats)");
     }
     e.ln_stats = (const float*)ln_stats->data_ptr();
     e.ln_colsum = (const float*)ln_colsum->data_ptr();

@@ -235,7 +235,8 @@ class VideoDepthAnything(nn.Module):
 
     Per-instance schedule switches (A/B experiments only; set before the first forward, they are part
     of the packed-weight cache key): ``fold_layernorms`` folds the encoder's norm1 / norm2 into the
-    qkv / fc1 GEMMs (fp16 mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
+    qkv / fc1 GEMMs and the motion modules' attention-block LayerNorms into their q/k/v GEMMs (fp16
+    mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
     proj / fc2 epilogues instead of a separate pass.  No environment variable changes the schedule."""
 
     fold_layernorms: bool = True
@@ -407,7 +408,7 @@ class VideoDepthAnything(nn.Module):
                              if ab.pos_encoder is not None else None)
                 # the LayerNorm folded into that GEMM (fp16, 'ape'; the forward takes it when a frame
                 # spans >= 256 rows): W' = gamma (.) W, colsum of the fp16 W', b' = W beta
-                a.fold = not fp32 and a.pe_bias is not None and (3 * Cm) % 256 == 0
+                a.fold = not fp32 and bool(self.fold_layernorms) and a.pe_bias is not None and (3 * Cm) % 256 == 0
                 if a.fold:
                     a.qkv_wg = (wqkv * nrm.weight.detach().float()[None, :]).half().contiguous().to(dev)
                     a.qkv_cs = a.qkv_wg.float().sum(1).contiguous()

@@ -330,6 +330,14 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
         bufs, rr_, work, _ = pend
         work.wait()  # the current stream (or, on gloo, the host) waits for the gather
         if rank == 0:
+            if strs:
+                # the receive buffers were allocated on a side stream, but the sink's D2H copies run on
+                # the current one: without this the caching allocator could hand their blocks to that
+                # side stream's next forward while the copies are still queued
+                cur_st = torch.cuda.current_stream(dev)
+                for b in bufs:
+                    if b.is_cuda:
+                        b.record_stream(cur_st)
             for src in range(world):
                 for j, r in enumerate(rr_):
                     k = r * world + src
