@@ -318,6 +318,10 @@ def main():
         }
         if gflop:
             line["model_tflops"] = round(value * gflop / 1e3, 1)
+            if roof is not None:
+                # the whole forward's algorithmic FLOPs at the measured frame rate, per GPU, against the
+                # dense fp16 peak (north_star's MFMA-utilisation bar), beside the dominant kernel's frac
+                roof["forward_frac"] = round(value / n_dev * gflop / 1e3 / PEAK_FP16_TFLOPS, 4)
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()

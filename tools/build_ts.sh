@@ -1,6 +1,6 @@
 #!/bin/bash
-# Instrumented build for tools/ts_probe.py: build/ts/{libvda.so, libvda_torch.so} with -DVDA_TS in the GEMM.
-# usage: bash tools/build_ts.sh ; VDA_LIB_OVERRIDE=build/ts/libvda.so python tools/ts_probe.py
+# Instrumented build for tools/ts_probe2.py: build/ts/{libvda.so, libvda_torch.so} with -DVDA_TS in the GEMM.
+# usage: bash tools/build_ts.sh ; VDA_LIB_OVERRIDE=build/ts/libvda.so python tools/ts_probe2.py
 set -e
 FL="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -I include -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form"
 D=build/ts; mkdir -p $D

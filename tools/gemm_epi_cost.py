@@ -28,6 +28,8 @@ def run(name, K, N, cfgs):
     w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
     b = torch.randn(N, device=dev) * 0.1
     stats = row_partials(x) if K == C else None
+    xf = x.float()
+    mr = torch.stack([xf.mean(1), torch.rsqrt(xf.var(1, unbiased=False) + 1e-6)], 1).contiguous() if K == C else None
     cs = w.float().sum(1).contiguous()
     res = torch.randn(M, N, device=dev).half()
     so = torch.empty(M, (N + 255) // 256, 2, device=dev)
@@ -36,7 +38,9 @@ def run(name, K, N, cfgs):
     for c in cfgs:
         e = _lib.Epilogue()
         e.bias = b.data_ptr(); e.rdiv = 1; e.rmod = 1
-        if "ln" in c:
+        if c.startswith("ln0"):  # finalized [M, 2] (mean, rstd)
+            e.ln_stats = mr.data_ptr(); e.ln_colsum = cs.data_ptr(); e.ln_parts = 0; e.ln_eps = 1e-6
+        elif "ln" in c:  # [M, 4, 2] partial sums, as the forward
             e.ln_stats = stats.data_ptr(); e.ln_colsum = cs.data_ptr(); e.ln_parts = 4; e.ln_eps = 1e-6
         if "gelu" in c:
             e.act = _lib.ACT_GELU
@@ -65,7 +69,7 @@ def run(name, K, N, cfgs):
                                                 for c, t in times.items()), flush=True)
 
 
-run("fc1", C, 4 * C, ["ln+gelu", "ln", "gelu", "bias"])
-run("qkv", C, 3 * C, ["ln", "bias"])
+run("fc1", C, 4 * C, ["ln+gelu", "ln0+gelu", "ln", "ln0", "gelu", "bias"])
+run("qkv", C, 3 * C, ["ln", "ln0", "bias"])
 run("proj", C, C, ["res+stats", "res", "bias"])
 run("fc2", 4 * C, C, ["res+stats", "res", "bias"])

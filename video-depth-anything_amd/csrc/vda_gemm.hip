@@ -1085,6 +1085,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         chain_dma(xn, wn2);
       }
     }
+    TS(4);
     static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
     const int g = lane >> 4;
     const long mrows = p.M - m0;
@@ -1712,7 +1713,7 @@ template <bool CONV, int ACT>
 int launch_act(const GemmParams& p, hipStream_t st) {  // returns the tile configuration it launched
   int cfg = g_force_tile;
   if (cfg < 0) {
-    // measured on MI355X (tools/bench_gemm.py): 256x256 wins every large-N shape; N = 128 prefers
+    // measured on MI355X (tools/archive/bench_gemm.py): 256x256 wins every large-N shape; N = 128 prefers
     // 256x128; short K (<= 256) and narrow N prefer the 2-blocks-per-CU 128x64 tile.
     const vda_epilogue& e = p.epi;
     const bool a16 = ((uintptr_t)p.y % 16 == 0) && p.ldy % 8 == 0 && p.N % 8 == 0 &&
@@ -1732,7 +1733,7 @@ int launch_act(const GemmParams& p, hipStream_t st) {  // returns the tile confi
     else if (CONV) cfg = 0;
     else {
       // small M (the streaming mode's one-frame encoder, M = 1,370): the largest tile that still
-      // gives >= 2 tiles per CU, else 64x64 (tools/bench_gemm_small.py: ViT-L fc2 72.8 -> 43.5 us,
+      // gives >= 2 tiles per CU, else 64x64 (tools/archive/bench_gemm_small.py: ViT-L fc2 72.8 -> 43.5 us,
       // proj 24.0 -> 14.0, qkv 29.5 -> 25.0, fc1 34.2 -> 30.3)
       const long ncu2 = 2L * cu_count();
       auto ntiles = [&](int bm, int bn) { return (long)((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };

@@ -375,7 +375,7 @@ bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout) {
   if ((long)BT * ((H + HC_TR - 1) / HC_TR) * ((W + HC_TC - 1) / HC_TC) > 0x7fffffffL) return false;
   if ((long)H * W * Cin >= (1L << 31) || (long)H * W * 512 >= (1L << 31)) return false;
   if (g_hconv_mode == 1) return true;
-  // measured (tools/bench_hconv.py, 32 frames): 148^2 1.26-1.29x, 74^2 1.07-1.11x, 37^2 0.73-0.76x the
+  // measured (tools/archive/bench_hconv.py, 32 frames): 148^2 1.26-1.29x, 74^2 1.07-1.11x, 37^2 0.73-0.76x the
   // implicit GEMM (a 37^2 map leaves 8 x 32 tiles 23 % empty and too few of them to fill the CUs)
   return (long)H * W >= 64L * 64L;
 }

@@ -302,7 +302,7 @@ def infer_video_depth(forward: Callable[[torch.Tensor], torch.Tensor], frames, t
     ``streams`` > 1 (GPU): consecutive window batches go round-robin onto that many HIP streams, so
     one window's forward can start while the previous one's tail kernels run (one GPU, two streams:
     the 176-frame ViT-L job in 414-420 ms against 442 ms on one stream and 413 ms for its 8 forwards
-    back to back; ``tools/video_probe.py``).  Each rank of a multi-GPU job does the same.
+    back to back; ``tools/archive/video_probe.py``).  Each rank of a multi-GPU job does the same.
     """
     if not isinstance(frames, torch.Tensor):
         frames = torch.from_numpy(np.ascontiguousarray(frames))
