@@ -410,6 +410,17 @@ __device__ __forceinline__ float gelu_tab(float x, unsigned phib) {
   return x * fmaf(x, ab.y, ab.x);
 }
 
+// LDS float2 access through asm (hipcc inserts no LDS-DMA alias wait for it); the read waits for itself
+__device__ __forceinline__ float2 lds_ld_f2(const float* ptr) {
+  float2 v;
+  asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v)
+               : "v"((unsigned)(uintptr_t)(VDA_LDS const float*)ptr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_st_f2(float* ptr, float2 v) {
+  asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)(VDA_LDS float*)ptr), "v"(v) : "memory");
+}
+
 __device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
 }
@@ -887,7 +898,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   // EK 3: the tile's (at most two) per-frame row-bias rows, 256 fp32 channels each, after the
   // statistics, in two slots by the parity of the block's tile index (a chaining epilogue stages the
   // next tile's rows while it still reads its own)
-  float* rb_lds = reinterpret_cast<float*>(lnst_lds + 4096);
+  float* rb_lds = reinterpret_cast<float*>(lnst_lds + 4096 + 1024);
   auto lnst_dma = [&](int m0_, int n0_, int vb_) {
     if constexpr (EK == 3) {
       if (wave < 2) {  // row 0 = the frame of tile row 0, row 1 = the next frame (rdiv >= 256: <= 2 per tile)
@@ -940,6 +951,37 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   }
   __builtin_amdgcn_s_barrier();
   TS(2);
+  // LNF: the tile's 256 (mean, rstd) pairs are formed ONCE here, one row per thread of waves 0-3, from
+  // the statistics the prologue staged (the producer's [M, P, 2] partial sums, or [M, 2] as is) into a
+  // 2-KiB [256][2] table the epilogue reads after the main loop's barriers: the epilogue's lanes no
+  // longer each reduce the partials of their 8 rows (4 lanes x 4 waves per row), and the staged
+  // statistics are free for the next tile's prologue DMA as soon as this pass has read them.
+  // The reads and the write go through asm: hipcc would put a vmcnt(0) before any LDS access here (a
+  // pending LDS-DMA may alias it), draining the previous tile's output stores at every tile start.  The
+  // statistics were retired by the prologue wait above and published by its barrier.
+  float* lnfin = reinterpret_cast<float*>(lnst_lds + 4096);
+  if constexpr (LNF && (EK == 1 || EK == 3)) {  // the register epilogues (the staged one reduces per row itself)
+    if (tid < 256) {
+      const float* st = reinterpret_cast<const float*>(lnst_lds);
+      const int P = p.epi.ln_parts;
+      const int sh = tid == lnst_shift_row(m0) ? 2 : 0;
+      float2 mr;
+      if (P <= 0) {
+        mr = lds_ld_f2(st + 2 * tid + sh);
+      } else {
+        float sm = 0.f, sq = 0.f;
+        for (int t = 0; t < P; ++t) {
+          const float2 pq = lds_ld_f2(st + 2 * (tid * P + t) + (t == P - 1 ? sh : 0));
+          sm += pq.x;
+          sq += pq.y;
+        }
+        const float invK = 1.f / (float)p.K;
+        const float mean = sm * invK;
+        mr = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq * invK), 0.f) + p.epi.ln_eps));
+      }
+      lds_st_f2(lnfin + 2 * tid, mr);
+    }
+  }
   // Dense GEMMs: the epilogue's per-channel bias / gamma are fetched now, under the main loop,
   // instead of costing a dependent L2/MALL round trip after it (convs: no VGPR room, loaded later).
   constexpr bool PREF = !CONV && !ROWB;
@@ -1047,33 +1089,19 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     const vda_epilogue& e = p.epi;
     const int rbslot = (vb / (int)gridDim.x) & 1;
     const int rbnd = EK == 3 ? e.rdiv - m0 % e.rdiv : 0;  // first tile row of the next frame
+    // The row statistics (lnfin) and the prefetched bias / colsum are taken into registers BEFORE the
+    // next tile's prologue DMA goes out: hipcc waits vmcnt(0) at their first use, which is free here
+    // and would drain that DMA after it.
     float2 mr[8];
     if constexpr (LNF) {
-      const float* st = reinterpret_cast<const float*>(lnst_lds);
-      const int P = e.ln_parts;
-      const float invK = 1.f / (float)p.K;
-      const int srow = lnst_shift_row(m0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int rl = wm * 128 + j * 16 + mcol;
-        const int sh = rl == srow ? 2 : 0;
-        if (P <= 0) {
-          mr[j] = *reinterpret_cast<const float2*>(st + 2 * rl + sh);
-        } else {
-          float sm = 0.f, sq = 0.f;
-#pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            const int tt = t < P ? t : 0;
-            const float2 pq = *reinterpret_cast<const float2*>(st + 2 * (rl * P + tt) + (tt == P - 1 ? sh : 0));
-            sm += t < P ? pq.x : 0.f;
-            sq += t < P ? pq.y : 0.f;
-          }
-          const float mean = sm * invK;
-          mr[j] = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq * invK), 0.f) + e.ln_eps));
-        }
-      }
+      for (int j = 0; j < 8; ++j) mr[j] = *reinterpret_cast<const float2*>(lnfin + 2 * (wm * 128 + j * 16 + mcol));
     }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // every LDS read of this tile (operands, statistics) is done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(pbv[i]), "v"(pgv[i]));
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's statistics reads have landed
+    // every LDS operand read of this tile is done (its MFMAs consumed them): hand the operand buffers
+    // and the staged statistics (already reduced into lnfin) to the next tile's prologue DMA
     __builtin_amdgcn_s_barrier();
     if constexpr (!CONV) {
       if (vb_next >= 0) {
@@ -1114,13 +1142,19 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           const int rl = wm * 128 + j * 16 + mcol;
           v[i] += *reinterpret_cast<const f4*>(rb_lds + rbslot * 512 + (rl >= rbnd ? 256 : 0) + wn * 64 + i * 16 + nq);
         }
-        if constexpr (ACT == VDA_ACT_GELU && TAB) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[i][r] = gelu_tab(v[i][r], phib);
-        } else if constexpr (ACT == VDA_ACT_GELU) {
+        if constexpr (ACT == VDA_ACT_GELU && !TAB) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[i][r] = gelu_erf(v[i][r]);
         }
+      }
+      if constexpr (ACT == VDA_ACT_GELU && TAB) {
+        // the row's 16 table lines are all requested before the first is used (one LDS round trip per
+        // row instead of a wait per group of reads)
+        phi_f2 ab[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ab[k] = phi_line(v[k / 4][k % 4], phib);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k / 4][k % 4] *= fmaf(v[k / 4][k % 4], ab[k].y, ab[k].x);
       }
       u32x4 o[2];
 #pragma unroll
@@ -1586,7 +1620,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
                                                       int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 : 0) +
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 + 1024 : 0) +
                                                      (EK == 2 ? 4096 : 0) + (EK == 3 ? 2048 : 0)];
   const int ntiles = tiles_m * tiles_n;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
