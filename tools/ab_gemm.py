@@ -47,6 +47,15 @@ def row_partials(y):  # [M, N] fp16 -> [M, ceil(N/256), 2] (sum, sumsq) fp32, as
 
 
 def mk(name):
+    if name == "ff1":  # a motion module's GEGLU feed-forward (the [h | g] interleaved W, N/2 outputs)
+        K, N = C, 8 * C
+        x = tok
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
+        b = torch.randn(N, device=dev) * 0.1
+        e = _lib.Epilogue()
+        e.bias = b.data_ptr(); e.rdiv = 1; e.rmod = 1; e.act = _lib.ACT_GEGLU
+        y = torch.empty(M, N // 2, device=dev, dtype=torch.float16)
+        return dict(x=x, w=w, y=y, e=e, K=K, N=N, keep=[x, w, b], res=None, ldy=N // 2)
     K, N = (C, 3 * C) if name == "qkv" else (C, C) if name == "proj" else (C, 4 * C) if name == "fc1" else (4 * C, C)
     x = tok if K == C else (torch.randn(M, K, device=dev) * 0.5).half()
     w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
@@ -67,7 +76,7 @@ def mk(name):
         keep += [res, so]
         e.res = res.data_ptr(); e.ldres = N; e.stats_out = so.data_ptr()
     y = torch.empty(M, N, device=dev, dtype=torch.float16)
-    return dict(x=x, w=w, y=y, e=e, K=K, N=N, keep=keep, res=res)
+    return dict(x=x, w=w, y=y, e=e, K=K, N=N, keep=keep, res=res, ldy=N)
 
 
 for name in shapes:
@@ -76,7 +85,7 @@ for name in shapes:
     for l in L:
         if s["res"] is not None:
             s["y"].copy_(s["res"]); s["e"].res = s["y"].data_ptr()  # in place, like the encoder
-        rc = l.vda_gemm(s["x"].data_ptr(), s["K"], s["w"].data_ptr(), s["y"].data_ptr(), s["N"], M, s["N"], s["K"],
+        rc = l.vda_gemm(s["x"].data_ptr(), s["K"], s["w"].data_ptr(), s["y"].data_ptr(), s["ldy"], M, s["N"], s["K"],
                         ctypes.byref(s["e"]), st)
         assert rc == 0, l.vda_last_error()
         torch.cuda.synchronize()
@@ -90,7 +99,7 @@ for name in shapes:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(n):
-                l.vda_gemm(s["x"].data_ptr(), s["K"], s["w"].data_ptr(), s["y"].data_ptr(), s["N"], M, s["N"], s["K"],
+                l.vda_gemm(s["x"].data_ptr(), s["K"], s["w"].data_ptr(), s["y"].data_ptr(), s["ldy"], M, s["N"], s["K"],
                            ctypes.byref(s["e"]), st)
             e1.record()
             torch.cuda.synchronize()

@@ -349,6 +349,19 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
     h8 pf[4];
     float t0, t1;
     auto expo = [&]() {
+#ifdef SA_TREE  // experiment: four interleaved partial sums (shorter add chains)
+      float u[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
+          u[kb * 2 + (r & 1)] += pv;
+          pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
+        }
+      t0 = u[0] + u[1];
+      t1 = u[2] + u[3];
+#else
       t0 = 0.f;
       t1 = 0.f;
 #pragma unroll
@@ -360,6 +373,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
           else t1 += pv;
           pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
         }
+#endif
     };
     if constexpr (FIRST) {
       rebase(tile_max());

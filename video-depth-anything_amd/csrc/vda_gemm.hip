@@ -405,15 +405,21 @@ __device__ __forceinline__ phi_f2 phi_line(float x, unsigned phib) {
   const float v = __builtin_amdgcn_fmed3f(fmaf(x, 128.f, PHI_MAGIC), PHI_LO, PHI_HI);
   return *(lds_cf2p)(uintptr_t)((__builtin_bit_cast(unsigned, v) << 3) + phib);
 }
-__device__ __forceinline__ float gelu_tab(float x, unsigned phib) {
-  const phi_f2 ab = phi_line(x, phib);
-  return x * fmaf(x, ab.y, ab.x);
-}
 
 // LDS float2 access through asm (hipcc inserts no LDS-DMA alias wait for it); the read waits for itself
 __device__ __forceinline__ float2 lds_ld_f2(const float* ptr) {
   float2 v;
   asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v)
+               : "v"((unsigned)(uintptr_t)(VDA_LDS const float*)ptr) : "memory");
+  return v;
+}
+__device__ __forceinline__ void lds_ld_f4x2(const float* ptr, float4& a, float4& b) {
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)" : "=v"(a), "=v"(b)
+               : "v"((unsigned)(uintptr_t)(VDA_LDS const float*)ptr) : "memory");
+}
+__device__ __forceinline__ float lds_ld_f1(const float* ptr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v)
                : "v"((unsigned)(uintptr_t)(VDA_LDS const float*)ptr) : "memory");
   return v;
 }
@@ -970,10 +976,17 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         mr = lds_ld_f2(st + 2 * tid + sh);
       } else {
         float sm = 0.f, sq = 0.f;
-        for (int t = 0; t < P; ++t) {
-          const float2 pq = lds_ld_f2(st + 2 * (tid * P + t) + (t == P - 1 ? sh : 0));
-          sm += pq.x;
-          sq += pq.y;
+        if (P == 4) {  // the encoder's 1024 channels: the row's 4 partials as two 16-B reads (P even: no shift)
+          float4 a, b;
+          lds_ld_f4x2(st + 8 * tid, a, b);
+          sm = ((a.x + a.z) + b.x) + b.z;
+          sq = ((a.y + a.w) + b.y) + b.w;
+        } else {
+          for (int t = 0; t < P; ++t) {
+            const float2 pq = lds_ld_f2(st + 2 * (tid * P + t) + (t == P - 1 ? sh : 0));
+            sm += pq.x;
+            sq += pq.y;
+          }
         }
         const float invK = 1.f / (float)p.K;
         const float mean = sm * invK;
@@ -1268,13 +1281,14 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       swap16_pair(ssq, x0, x1); ssq = x0 + x1;
       swap32_pair(ssum, x0, x1); ssum = x0 + x1;
       swap32_pair(ssq, x0, x1); ssq = x0 + x1;
-      if (g == 0) *reinterpret_cast<float2*>(red + 2 * (wn * 256 + rl)) = make_float2(ssum, ssq);
+      if (g == 0) lds_st_f2(red + 2 * (wn * 256 + rl), make_float2(ssum, ssq));  // asm: no LDS-DMA vmcnt
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_s_barrier();
     {  // thread -> (row, statistic): the 4 column-slices of the 256-column block, in a fixed order
       const int row = tid >> 1, st = tid & 1;
-      const float v = red[2 * row + st] + red[2 * (256 + row) + st] + red[2 * (512 + row) + st] + red[2 * (768 + row) + st];
+      const float v = lds_ld_f1(red + 2 * row + st) + lds_ld_f1(red + 2 * (256 + row) + st) +
+                      lds_ld_f1(red + 2 * (512 + row) + st) + lds_ld_f1(red + 2 * (768 + row) + st);
       const int P = (p.N + 255) / 256;
       const int m = m0 + row;
       const __amdgpu_buffer_rsrc_t rs =
@@ -1386,6 +1400,23 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           }
         }
     }
+    if constexpr (ACT == VDA_ACT_GEGLU && TAB) {
+      // the gate halves (accumulators 1 and 3) through the table GELU in place, 16 values per step with
+      // all 16 LDS reads issued before the first is consumed (as the GELU pass above)
+#pragma unroll
+      for (int i = 1; i < 4; i += 2)
+#pragma unroll
+        for (int j = 0; j < 8; j += 4) {
+          phi_f2 ab[16];
+#pragma unroll
+          for (int k = 0; k < 16; ++k) ab[k] = phi_line(acc[i][j + k / 4][k % 4], phib);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) {
+            const float a = acc[i][j + k / 4][k % 4];
+            acc[i][j + k / 4][k % 4] = a * fmaf(a, ab[k].y, ab[k].x);
+          }
+        }
+    }
     auto phase1 = [&](auto g_tag) {
       constexpr bool HG = decltype(g_tag)::value;
 #pragma unroll
@@ -1404,7 +1435,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
           if constexpr (ACT == VDA_ACT_GEGLU) {
             const f4 vh = acc[i][j], vg = acc[i + 1][j];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? gelu_tab(vg[r], phib) : gelu_erf(vg[r]));
+            for (int r = 0; r < 4; ++r) v[r] = vh[r] * (TAB ? vg[r] : gelu_erf(vg[r]));  // TAB: gate done above
             col = ((wn * 64 + i * 16) >> 1) + nq;
           } else {
             v = acc[i][j];
@@ -1663,7 +1694,10 @@ VDA_KNOB(int, g_desync, 0);       // vda_debug_gemm_desync
 // vda_debug_gemm_epi: the residual + row-statistics GEMMs (proj / fc2) through the register epilogue
 // (EK 2).  Off: bit-identical but measured slower than the staged epilogue (proj 94.8 -> 102.9 us,
 // fc2 320 -> 334 us at 43840 rows, same box, tools/ab_gemm.py).
-VDA_KNOB(int, g_res_epi, 0);
+#ifndef VDA_RES_EPI_DEFAULT
+#define VDA_RES_EPI_DEFAULT 0
+#endif
+VDA_KNOB(int, g_res_epi, VDA_RES_EPI_DEFAULT);
 
 int cu_count() { return vda_cu_count(); }
 
@@ -1673,6 +1707,12 @@ void phased_sched(int ntiles, int nk, bool conv, int& grid, int& ticks) {
   // measured in situ: persistent pays for the dense GEMMs, one block per tile for the convs
   const int persist = conv ? 0 : (g_persist >= 0 ? g_persist : cus);
   grid = persist == 0 ? ntiles : std::min(ntiles, persist);
+#ifdef VDA_RIGHTSIZE  // experiment: the fewest blocks that keep the round count (the rest of the CUs stay free)
+  if (persist > 0 && ntiles > grid) {
+    const int rounds = (ntiles + grid - 1) / grid;
+    grid = (ntiles + rounds - 1) / rounds;
+  }
+#endif
   // The start stagger for a short last round (half the blocks with one tile fewer start half a
   // tile late, ~1.45 us per 64-deep K step + ~6 us prologue/epilogue) is off by default: it is worth
   // +0.4 % with one clip in flight but -0.6 % with the two clips in flight the drivers run (the
