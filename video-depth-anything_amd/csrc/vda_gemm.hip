@@ -1208,8 +1208,8 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
   }
   if constexpr (EK == 2 && XR == 2 && WR == 2) {
     // Register epilogue with one residual and the row statistics (proj, fc2: x += ...): the residual
-    // rows are requested first (in the same 8-consecutive-channel layout the permlane swap produces),
-    // then the operand buffers are handed to the next tile's prologue DMA as above.  Output =
+    // rows are requested first (in the whole-line layout the stores use, below), then the operand
+    // buffers are handed to the next tile's prologue DMA as above.  Output =
     // fp16(acc + bias) + residual in packed fp16, as the staged epilogue.  Row statistics: (sum, sumsq)
     // of the stored fp16 values per lane, over the 4 lanes of a row by permlane swaps, over the 4 waves
     // of a 256-column block through an 8-KiB LDS table.
@@ -1227,14 +1227,22 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       ccol[pp] = n0 + wn * 64 + 32 * pp + 16 * (g & 1) + 8 * (g >> 1);
       cok[pp] = ccol[pp] < p.N;
     }
+    // Whole 128-B lines, as the EK 1 epilogue: after the permlane swap a lane holds 8 consecutive
+    // channels of its row mcol; a DPP row_ror:8 exchange between lanes l and l ^ 8 then gives every lane
+    // 8 channels of row mcol & 7 (A) and of row 8 + (mcol & 7) (B) at one column offset, so each 16-B
+    // store (and each residual load, requested in that layout up front) covers whole lines.
+    const bool lo8 = (mcol & 8) == 0;
+    const int colx = lo8 ? ccol[0] : ccol[1];
+    const bool cokx = lo8 ? cok[0] : cok[1];
     const __amdgpu_buffer_rsrc_t rr = rsrc_rows(e.res, e.ldres);
     h8 rv[8][2];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
-      for (int pp = 0; pp < 2; ++pp) {
-        const unsigned o = cok[pp] ? (unsigned)((((long)(wm * 128 + j * 16 + mcol)) * e.ldres + ccol[pp]) * 2) : 0x80000000u;
-        rv[j][pp] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
+      for (int ab = 0; ab < 2; ++ab) {
+        const long row = wm * 128 + j * 16 + (mcol & 7) + 8 * ab;
+        const unsigned o = cokx ? (unsigned)((row * e.ldres + colx) * 2) : 0x80000000u;
+        rv[j][ab] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr, o, 0, 0));
       }
     __builtin_amdgcn_s_barrier();  // every wave is done reading the operand buffers
     if constexpr (!CONV) {
@@ -1252,7 +1260,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int rl = wm * 128 + j * 16 + mcol;
-      float ssum = 0.f, ssq = 0.f;
+      u32x4 o[2];
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp) {
         float a[4], c[4];
@@ -1265,16 +1273,29 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
         typedef float f2v __attribute__((ext_vector_type(2)));
         const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
         const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
-        const h8 t = __builtin_bit_cast(h8, make_uint4(__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
-                                                       __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3))) +
-                     rv[j][pp];
-        const unsigned o = cok[pp] ? (unsigned)((((long)rl) * p.ldy + ccol[pp]) * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, o, 0, VDA_EPI_STORE_AUX);
-        float s1, q1;
-        stat_acc(cok[pp] ? t : h8{0, 0, 0, 0, 0, 0, 0, 0}, s1, q1);
-        ssum += s1;
-        ssq += q1;
+        o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                      __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
       }
+      u32x4 A, B;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned snd = lo8 ? o[1][k] : o[0][k];
+        const unsigned got = (unsigned)__builtin_amdgcn_mov_dpp((int)snd, 0x128, 0xF, 0xF, true);
+        A[k] = lo8 ? o[0][k] : got;
+        B[k] = lo8 ? got : o[1][k];
+      }
+      const h8 tA = __builtin_bit_cast(h8, A) + rv[j][0];
+      const h8 tB = __builtin_bit_cast(h8, B) + rv[j][1];
+      const unsigned rA = cokx ? (unsigned)(((long)(wm * 128 + j * 16 + (mcol & 7)) * p.ldy + colx) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tA), ry, rA, 0, VDA_EPI_STORE_AUX);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tB), ry, rA + (unsigned)(8 * p.ldy * 2), 0,
+                                             VDA_EPI_STORE_AUX);
+      float sA, qA, sB, qB;
+      stat_acc(cokx ? tA : h8{0, 0, 0, 0, 0, 0, 0, 0}, sA, qA);
+      stat_acc(cokx ? tB : h8{0, 0, 0, 0, 0, 0, 0, 0}, sB, qB);
+      // lane l keeps row mcol (l < 8 of its 16: A, else B) and adds its partner l ^ 8's piece of that row
+      float ssum = (lo8 ? sA : sB) + dpp_f<0x128>(lo8 ? sB : sA);
+      float ssq = (lo8 ? qA : qB) + dpp_f<0x128>(lo8 ? qB : qA);
       // the row's 64 channels of this wave sit in lanes mcol, mcol + 16, + 32, + 48
       float x0, x1;
       swap16_pair(ssum, x0, x1); ssum = x0 + x1;
@@ -1692,8 +1713,11 @@ VDA_KNOB(int, g_persist, -1);     // vda_debug_gemm_sched; -1 = automatic
 VDA_KNOB(int, g_stagger, -1);
 VDA_KNOB(int, g_desync, 0);       // vda_debug_gemm_desync
 // vda_debug_gemm_epi: the residual + row-statistics GEMMs (proj / fc2) through the register epilogue
-// (EK 2).  Off: bit-identical but measured slower than the staged epilogue (proj 94.8 -> 102.9 us,
-// fc2 320 -> 334 us at 43840 rows, same box, tools/ab_gemm.py).
+// (EK 2).  Off: bit-identical but measured slower than the staged epilogue (round 3: proj 94.8 -> 102.9
+// us, fc2 320 -> 334 us; round 4 with whole-line stores / residual loads and asm LDS statistics: proj
+// 104.9 -> 111.9, fc2 319.2 -> 331.2, same box, tools/ab_gemm.py, profiles/r04_ab_gemm_ek2.log): the
+// residual loads issued at the epilogue start are waited for right away, where the staged epilogue
+// covers them with its LDS staging pass.
 #ifndef VDA_RES_EPI_DEFAULT
 #define VDA_RES_EPI_DEFAULT 0
 #endif
