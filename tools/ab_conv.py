@@ -4,6 +4,7 @@ usage: python tools/ab_conv.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes oc
 oc1:    output_conv1, 3x3 256 -> 128 on the x2 bilinear resize of a [32, 148, 148, 256] map (fused)
 depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
 rcu148: refinenet1 RCU conv, 3x3 256 -> 256 at 148^2 with pre-ReLU + ReLU
+l3rn / l4rn: layer3_rn / layer4_rn, 3x3 1024 -> 256 (no bias) at 37^2 / 19^2 (the strip conv; 19^2 splits)
 Outputs compared bit-for-bit against the first library's.
 """
 import ctypes
@@ -58,6 +59,20 @@ def case(name):
             return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 256, 3, 1, 1, 1, 0, 0,
                                 ctypes.byref(e), None, 0, st)
         return run, y, fl, [x, w, b, e]
+    if name in ("l3rn", "l4rn"):
+        S = 37 if name == "l3rn" else 19
+        x = (torch.randn(32, S, S, 1024, device=dev) * 0.5).half()
+        w = (torch.randn(256, 3, 3, 1024, device=dev) * (9 * 1024) ** -0.5).half()
+        y = torch.empty(32, S, S, 256, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1)
+        fl = 2.0 * 32 * S * S * 256 * 9216
+        nb = max(L[0].vda_conv2d_workspace(32, S, S, 1024, 256, 3, 1, 1), 16)
+        ws = torch.empty(nb, device=dev, dtype=torch.uint8)
+
+        def run(l):
+            return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, S, S, 1024, 256, 3, 1, 1, 0, 0, 0,
+                                ctypes.byref(e), ws.data_ptr(), nb, st)
+        return run, y, fl, [x, w, e, ws]
     x = (torch.randn(32, 296, 296, 128, device=dev) * 0.5).half()
     w32 = torch.randn(32, 3, 3, 128, device=dev) * (9 * 128) ** -0.5
     w1 = torch.cat([w32.half(), (w32 - w32.half().float()).half()], 0).contiguous()

@@ -1,10 +1,11 @@
 """In-process A/B of the encoder GEMMs across libvda builds (tuning tool, not product code).
 
-usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes qkv,proj,fc1,fc2]
+usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes qkv,proj,fc1,fc2] [--m M]
 
 Each library is loaded through ctypes and called through the C ABI (vda_gemm) on the current torch
 stream with the forward's exact epilogues (LN fold from [M, 4, 2] partials for qkv / fc1, residual +
-row statistics for proj / fc2).  Rounds alternate the libraries (one process, one device), and every
+row statistics for proj / fc2).  `--m` changes the token count (default 43,840 = the forward's; e.g.
+32,768 makes proj / fc2 exactly two rounds of 256x256 tiles on 256 CUs).  Rounds alternate the libraries (one process, one device), and every
 output is compared bit-for-bit against the first library's.
 """
 import ctypes
@@ -17,12 +18,14 @@ import torch
 from vda_amd import _lib
 
 args = sys.argv[1:]
-rounds, shapes = 7, ["qkv", "proj", "fc1", "fc2"]
+rounds, shapes, M = 7, ["qkv", "proj", "fc1", "fc2"], 43840
 libs = []
 i = 0
 while i < len(args):
     if args[i] == "--rounds":
         rounds = int(args[i + 1]); i += 2
+    elif args[i] == "--m":
+        M = int(args[i + 1]); i += 2
     elif args[i] == "--shapes":
         shapes = args[i + 1].split(","); i += 2
     else:
@@ -36,7 +39,7 @@ for k, p in enumerate(libs):
 
 dev = "cuda"
 torch.manual_seed(0)
-M, C = 43840, 1024
+C = 1024
 tok = (torch.randn(M, C, device=dev) * 2).half()
 st = torch.cuda.current_stream().cuda_stream
 

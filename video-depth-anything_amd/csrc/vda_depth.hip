@@ -32,6 +32,7 @@ constexpr int DNPIX = DP * DP;      // 324
 __device__ __forceinline__ void dh_glds16(const void* src, h16* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
 }
+typedef unsigned dh_u4 __attribute__((ext_vector_type(4)));
 template <int N>
 __device__ __forceinline__ void dh_wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -197,8 +198,14 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       const uint4 z = make_uint4(0u, 0u, 0u, 0u);
       const uint4 o = ok ? __builtin_bit_cast(uint4, v) : z;
       const int slot = LIN ? p * PSTR + pos : s;
-      if (k + 1 < UCH || s < USL) *reinterpret_cast<uint4*>(patch + (u & 1) * PBUF + slot * 8) = o;
+      // asm store: a compiler-visible LDS store that may alias the LDS-DMA ring gets an s_waitcnt
+      // vmcnt(0) in front of it, which drained the next step's weight DMA before the interpolation
+      if (k + 1 < UCH || s < USL)
+        asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)(VDA_LDS h16*)(patch + (u & 1) * PBUF + slot * 8)),
+                     "v"(__builtin_bit_cast(dh_u4, o))
+                     : "memory");
     }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the stores above are invisible to the compiler's counts
   };
   // weight pieces of step st of a unit of slab `slab` -> ring slot `wslot`
   auto dma_w = [&](int st, int slab, int wslot) {
@@ -245,6 +252,12 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   for (int a = 0; a < NB; ++a)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+  // the plain conv's bias, held for the whole launch (a lane's channels do not change with the tile): a
+  // load in the epilogue made every tile end wait (vmcnt(0)) for it
+  f4 bias_r[DEPTH ? 1 : NB];
+#pragma unroll
+  for (int a = 0; a < (DEPTH ? 1 : NB); ++a)
+    bias_r[a] = (!DEPTH && b1) ? *reinterpret_cast<const f4*>(b1 + (ng * NB + a) * 16 + g * 4) : f4{0.f, 0.f, 0.f, 0.f};
   const int my_pp = (PP - 1 - wave) / 8 + 1;             // next-slab patch pieces of this wave
   constexpr int PPMAX = (PP + 7) / 8;
   float pend[4] = {0.f, 0.f, 0.f, 0.f};
@@ -338,7 +351,7 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
 #pragma unroll
       for (int a = 0; a < NB; ++a) {
         const int n = (ng * NB + a) * 16 + g * 4;
-        const f4 bv = b1 ? *reinterpret_cast<const f4*>(b1 + n) : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 bv = bias_r[DEPTH ? 0 : a];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int y = y0 + mg * 4 + i, x = x0 + frow;

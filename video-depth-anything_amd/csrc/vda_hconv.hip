@@ -11,7 +11,7 @@
 // X tile is refetched 9 times per 64-channel slab, and with Cout = 256 there is a single N tile, so
 // nothing else amortises those bytes (~5x the map in fabric reads, K steps at ~2x the dense GEMM's).
 // Here a block owns an 8 x 32 output tile (256 pixels) and stages its 10 x 34 input patch ONCE per
-// 64-channel slab by LDS-DMA (43 KiB, spread over the first 6 K steps of the previous slab); all 9
+// 64-channel slab by LDS-DMA (48 KiB, spread over the first 6 K steps of the previous slab); all 9
 // taps read their X fragments out of the patch at a tap offset.  Per K step (one tap of one slab)
 // only the 32-KiB W tile is streamed, exactly as in the dense phased GEMM:
 //
@@ -22,20 +22,25 @@
 //   issued in P1 of steps 0..5 of slab s and retired by the same step's P4 wait; the slot they fill
 //   was last read in P3 of the previous slab's last step (2 phases earlier, the stagger margin).
 //
-// LDS: 2 x 32 KiB W + 2 x 43 KiB patch = 150 KiB; the fp16 output tile (128 KiB) is staged over it
-// in the epilogue and written as whole 512-B pixel rows.  Patch slot layout: pixel p's 16-B chunk c
-// at p * 128 B + ((c ^ (p & 7)) * 16): for the ds_read_b128 lane groups (16 consecutive pixels of
-// one tile row, chunks c / c + 1) the 16 accesses of a group hit 16 distinct (p & 1, chunk ^ (p & 7))
-// bank quads at any tap offset, i.e. conflict-free.
+// LDS: 2 x 32 KiB W + 2 x 48 KiB patch = 160 KiB; the fp16 output tile (128 KiB) is staged over it
+// in the epilogue and written as whole 512-B pixel rows.  Patch slot layout (round 4): linear, pixel p's
+// 16-B chunk c at (p * 9 + c) * 16 B (8 chunks + 1 pad slot per pixel), so a tap moves every X fragment
+// read by one scalar and the rest of the address is a lane constant + immediates: the XOR-swizzled
+// layout it replaces (p * 128 B + ((c ^ (p & 7)) * 16), conflict-free) cost ~40 VALU of address math per
+// quadrant, 2.6 VALU per MFMA against the dense GEMM's 1.7 (profiles/r04_pmc_conv_gemm.log); the 9-slot
+// stride leaves the ds_read_b128 lane groups 2-way conflicted at worst (10 slots would be conflict-free
+// but do not fit the LDS).
 #include "vda_common.h"
 #include "../../include/vda.h"
+#include <type_traits>
 
 namespace {
 
 constexpr int HC_TR = 8, HC_TC = 32;                 // output tile rows x columns
 constexpr int HC_PC = HC_TC + 2;                     // patch width (34)
 constexpr int HC_NPIX = (HC_TR + 2) * HC_PC;         // 340 patch pixels
-constexpr int HC_PP = (HC_NPIX * 8 + 63) / 64;       // 43 one-KiB DMA pieces per 64-channel slab
+constexpr int HC_PSTR = 9;                           // 16-B slots per patch pixel (8 channel chunks + 1 pad)
+constexpr int HC_PP = (HC_NPIX * HC_PSTR + 63) / 64; // 48 one-KiB DMA pieces per 64-channel slab
 constexpr int HC_PSLOT = HC_PP * 512;                // halfs per patch slot
 constexpr int HC_PPW = (HC_PP + 7) / 8;              // patch pieces per wave (6; waves 3-7 own 5)
 constexpr int HC_BK = 64;
@@ -44,6 +49,14 @@ constexpr int HC_WBUF = 2 * HC_HALF;                 // one K step of W (256 row
 static_assert(HC_PPW <= 9, "patch pieces are issued in the first steps of a slab");
 
 __device__ __attribute__((aligned(64))) uint4 g_hc_zero[4];
+
+#ifdef VDA_TS  // per-block phase timestamps (tools/ts_hconv.py; experiments only): kept in registers and
+               // stored once at the block's end, so the stamps add no memory operation inside the block
+__device__ unsigned long long g_hts[8192][6];
+#define HTS(k) (hts[k] = __builtin_amdgcn_s_memrealtime())
+#else
+#define HTS(k) ((void)0)
+#endif
 
 __device__ __forceinline__ int hc_swz(int row, int chunk) { return row * HC_BK + ((chunk ^ ((row >> 1) & 7)) << 3); }
 
@@ -67,6 +80,10 @@ struct HconvArgs {
 template <bool PRE>
 __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   __shared__ __attribute__((aligned(1024))) h16 smem[2 * HC_WBUF + 2 * HC_PSLOT];
+#ifdef VDA_TS
+  unsigned long long hts[6];
+#endif
+  HTS(0);
   h16* const wsm = smem;
   h16* const psm = smem + 2 * HC_WBUF;
 
@@ -96,22 +113,28 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   const h16* xf0 = a.x + (long)bt * H * W * Cin;
 
   // this lane's patch pieces: element offset (slab 0) within the frame, -1 = zero (padding / unused)
+  // (linear patch: slot s = pixel * HC_PSTR + chunk, the pad slot and the pixels past the map read zeros)
   int poff[HC_PPW];
 #pragma unroll
   for (int j = 0; j < HC_PPW; ++j) {
     const int q = wave + 8 * j;
-    const int p = q * 8 + (lane >> 3);
-    const int cd = (lane & 7) ^ (p & 7);
+    const int sl = q * 64 + lane;
+    const int p = sl / HC_PSTR, cd = sl - p * HC_PSTR;
     const int pr = p / HC_PC, pc = p - pr * HC_PC;
     const int iy = y0 - 1 + pr, ix = x0 - 1 + pc;
-    poff[j] = (q < HC_PP && p < HC_NPIX && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+    poff[j] = (q < HC_PP && p < HC_NPIX && cd < 8 && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
                   ? (iy * W + ix) * Cin + cd * 8
                   : -1;
   }
+  // the zero page's address is laundered once: left to the compiler, its GOT load sits in every piece's
+  // conditional block, with an lgkmcnt(0) that also waits for the phase's fragment reads
+  uint64_t zpa = (uint64_t)(uintptr_t)g_hc_zero;
+  asm volatile("" : "+s"(zpa));
+  const void* const zero = (const void*)(uintptr_t)zpa;
   auto patch_piece = [&](int slab, int j) {
     const int q = wave + 8 * j;
     if (q < HC_PP) {
-      const void* src = poff[j] >= 0 ? (const void*)(xf0 + poff[j] + slab * 64) : (const void*)g_hc_zero;
+      const void* src = poff[j] >= 0 ? (const void*)(xf0 + poff[j] + slab * 64) : zero;
       __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)(psm + (slab & 1) * HC_PSLOT + q * 512), 16, 0, 0);
     }
   };
@@ -146,6 +169,12 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  // the epilogue's bias, requested before the prologue: loaded in the epilogue, each of the four f4
+  // loads was waited for (vmcnt(0)) right after the main loop
+  f4 bias_r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    bias_r[i] = a.bias ? *reinterpret_cast<const f4*>(a.bias + wn * 64 + i * 16 + (lane >> 4) * 4) : f4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: slab 0's patch, all of W(0), W(1) quarter 1 (the loop expects it from "step -1")
 #pragma unroll
@@ -162,16 +191,14 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   // PRE (the RCU's relu(x) input): the patch is rectified once in LDS after it lands (2 passes per
   // slab in P2 of the slab's steps 7 and 8, 3 16-B slots per thread each), not per fragment read
   // (each patch value feeds 9 taps x 4 n-waves)
+  static_assert(HC_PP * 64 == 6 * 512, "relu pass: two passes of 3 slots per thread cover the patch exactly");
   auto relu_pass = [&](int slot, int part) {
-    h16* ps = psm + slot * HC_PSLOT;
+    h8* ps = reinterpret_cast<h8*>(psm + slot * HC_PSLOT) + tid + 512 * 3 * part;
+    h8 v[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int sl = tid + 512 * (3 * part + k);
-      if (sl < HC_PP * 64) {
-        h8* pp = reinterpret_cast<h8*>(ps + sl * 8);
-        *pp = relu8(*pp);
-      }
-    }
+    for (int k = 0; k < 3; ++k) v[k] = ps[512 * k];  // all three reads in flight before the first write
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ps[512 * k] = relu8(v[k]);
   };
   if (PRE) {
     relu_pass(0, 0);
@@ -179,6 +206,7 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
   }
+  HTS(1);
   const bool lagging = wave >= 4;
   if (lagging) __builtin_amdgcn_s_barrier();
 
@@ -187,17 +215,21 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   const int wrow0 = (wn & 1) * 64;
   h8 xf[4][2], wf[2][2];
   // X fragments of quadrant qm (m-blocks wm*8 + qm*4 + j = tile row wm*4 + qm*2 + (j >> 1), columns
-  // (j & 1) * 16 + frow) at tap offset toff = dy * 34 + dx, from patch slot ps
+  // (j & 1) * 16 + frow) at tap offset toff = dy * 34 + dx.  The linear layout makes every read one
+  // lane-constant byte offset + the tap's scalar offset + an immediate (the swizzled layout needed ~40
+  // VALU of address math per quadrant); the 9-slot pixel stride leaves the ds_read_b128 lane groups
+  // 2-way conflicted at worst (10 would be conflict-free but does not fit the LDS).
+  const unsigned xlane = (unsigned)(((wm * 4 * HC_PC + frow) * HC_PSTR + fchunk) * 16);
   auto load_x = [&](const h16* ps, int toff, int qm) {
+    unsigned tb;  // patch slot + tap offset, opaque (one VALU add per quadrant, the rest immediates)
+    asm volatile("s_mov_b32 %0, %1" : "=s"(tb) : "s"((unsigned)((uintptr_t)(VDA_LDS const h16*)ps) + (unsigned)(toff * HC_PSTR * 16)));
+    const VDA_LDS char* xb = reinterpret_cast<const VDA_LDS char*>((uintptr_t)(tb + xlane));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int p = (wm * 4 + qm * 2 + (j >> 1)) * HC_PC + (j & 1) * 16 + frow + toff;
-      const int c0 = fchunk ^ (p & 7);
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        xf[j][ks] = *reinterpret_cast<const h8*>(&ps[p * 64 + ((c0 ^ (4 * ks)) << 3)]);
-      }
-    }
+      for (int ks = 0; ks < 2; ++ks)
+        xf[j][ks] = *reinterpret_cast<const VDA_LDS h8*>(
+            xb + ((qm * 2 + (j >> 1)) * HC_PC + (j & 1) * 16) * HC_PSTR * 16 + ks * 64);
   };
   auto load_w = [&](const h16* base, int qn) {
 #pragma unroll
@@ -223,41 +255,48 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     __builtin_amdgcn_s_barrier();
   };
 
-  for (int kt = 0; kt < NK; ++kt) {
-    const int cb = kt & 1, nb = cb ^ 1;
-    const int slab = kt / 9, tap = kt - slab * 9;
-    const int toff = (tap / 3) * HC_PC + (tap % 3);
+  // the 9 taps of a slab unrolled: tap offsets, patch-piece and relu-pass slots are compile-time (the
+  // rolled loop's per-step tap / slab division and the run-time piece select cost 824 -> 717 us on
+  // refinenet1's RCU conv, bit-identical; profiles/r04_ab_hconv.log).  Per step, 4 phases:
+  // P1 (+ one piece of the next slab's patch in steps 0..HC_PPW-1), P2 (+ the next step's W quarter,
+  // the relu pass of the next slab in steps 7 / 8), P3, P4 (retire everything but this phase's W(t+2))
+  for (int slab = 0; slab < nslab; ++slab) {
     const h16* ps = psm + (slab & 1) * HC_PSLOT;
-    const h16* base = wsm + cb * HC_WBUF;
-    const bool more1 = kt + 1 < NK, more2 = kt + 2 < NK;
-    // P1 (+ one piece of the next slab's patch in steps 0..HC_PPW-1)
-    load_x(ps, toff, 0);
-    load_w(base, 0);
-    if (tap < HC_PPW && slab + 1 < nslab) {
-#pragma unroll
-      for (int j = 0; j < HC_PPW; ++j)
-        if (j == tap) patch_piece(slab + 1, j);
-    }
-    mma(0, 0);
-    // P2
-    load_w(base, 1);
-    if (more1) stage_w(kt + 1, nb, 0);
-    if (PRE && tap >= 7 && slab + 1 < nslab) relu_pass((slab + 1) & 1, tap - 7);
-    mma(0, 1);
-    // P3
-    load_x(ps, toff, 1);
-    mma(1, 1);
-    // P4: retire everything but this phase's W(t+2) quarter
-    load_w(base, 0);
-    if (more2) {
-      stage_w(kt + 2, cb, 1);
-      hc_wait<2>();
-    } else {
-      hc_wait<0>();
-    }
-    mma(1, 0);
+    const bool nxt = slab + 1 < nslab;
+    auto step = [&](auto tap_c) {
+      constexpr int tap = decltype(tap_c)::value;
+      constexpr int toff = (tap / 3) * HC_PC + (tap % 3);
+      const int kt = slab * 9 + tap;
+      const int cb = kt & 1, nb = cb ^ 1;
+      const h16* base = wsm + cb * HC_WBUF;
+      const bool more1 = kt + 1 < NK, more2 = kt + 2 < NK;
+      load_x(ps, toff, 0);
+      load_w(base, 0);
+      if (tap < HC_PPW && nxt) patch_piece(slab + 1, tap < HC_PPW ? tap : 0);
+      mma(0, 0);
+      load_w(base, 1);
+      if (more1) stage_w(kt + 1, nb, 0);
+      if (PRE && tap >= 7 && nxt) relu_pass((slab + 1) & 1, tap >= 7 ? tap - 7 : 0);
+      mma(0, 1);
+      load_x(ps, toff, 1);
+      mma(1, 1);
+      load_w(base, 0);
+      if (more2) {
+        stage_w(kt + 2, cb, 1);
+        hc_wait<2>();
+      } else {
+        hc_wait<0>();
+      }
+      mma(1, 0);
+    };
+    step(std::integral_constant<int, 0>{}); step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{}); step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{}); step(std::integral_constant<int, 5>{});
+    step(std::integral_constant<int, 6>{}); step(std::integral_constant<int, 7>{});
+    step(std::integral_constant<int, 8>{});
   }
   if (!lagging) __builtin_amdgcn_s_barrier();
+  HTS(2);
   __syncthreads();
 
   // ---- epilogue: +bias [ReLU] -> fp16 [256 px][256 ch] image in LDS (8-byte units XOR-swizzled by
@@ -266,7 +305,7 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int col = wn * 64 + i * 16 + nq;
-    const f4 bv = a.bias ? *reinterpret_cast<const f4*>(a.bias + col) : f4{0.f, 0.f, 0.f, 0.f};
+    const f4 bv = bias_r[i];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int ml = wm * 128 + j * 16 + mcol;
@@ -284,6 +323,7 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     }
   }
   __syncthreads();
+  HTS(3);
   // thread -> 16-B chunk q of pixels row0 + 16 it (it = 0..15): tile row it >> 1, column row0 + 16 (it & 1)
   const int q = tid & 31, row0 = tid >> 5;
   const h16* l0 = smem + row0 * 256 + ((2 * q) ^ row0) * 4;
@@ -362,6 +402,13 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     }
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), ry, vo, 0, 2);
   }
+#ifdef VDA_TS
+  HTS(4);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  HTS(5);
+  if (tid == 0 && blockIdx.x < 8192)
+    for (int k = 0; k < 6; ++k) g_hts[blockIdx.x][k] = hts[k];
+#endif
 }
 
 }  // namespace
@@ -401,6 +448,11 @@ int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int
   return 0;
 }
 
+#ifdef VDA_TS
+extern "C" int vda_debug_hconv_timestamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_hts), sizeof(g_hts), 0, hipMemcpyDeviceToHost);
+}
+#endif
 #ifdef VDA_TUNING
 extern "C" int vda_debug_hconv(int32_t mode) {
   g_hconv_mode = mode;
