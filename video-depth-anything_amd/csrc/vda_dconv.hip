@@ -59,8 +59,6 @@ __device__ __forceinline__ void dc_wait_n(int n) {  // n: wave-uniform, 0..9
 // lgkmcnt(0) as the builtin (vmcnt / expcnt untouched): the compiler then knows the fragments read
 // before it are complete and adds no wait of its own for them after later reads
 __device__ __forceinline__ void dc_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
-typedef unsigned dc_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ unsigned dc_lds_addr(const h16* p) { return (unsigned)(uintptr_t)(VDA_LDS const h16*)p; }
 
 // UPS: U is the map BEFORE the bilinear (align_corners=True) resize from (Hs, Ws) to (H, W); each
 // unit's patch is interpolated in LDS from a staged source region (bilerp8, the resize kernel's
@@ -196,23 +194,13 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
           sx0 = (int)fx; sx1 = min(sx0 + 1, Ws - 1); wx = fx - (float)sx0;
         }
         const int r0 = (sy0 - sy_lo) * SC, r1 = (sy1 - sy_lo) * SC, c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
-        // the source reads and the patch store in asm: as compiler-visible LDS accesses that may alias
-        // a LDS-DMA target they got an s_waitcnt vmcnt(0) in front, i.e. waited for this phase's weight
-        // DMA (the source itself landed by the row-0 wait and barrier); callers wait lgkmcnt(0)
-        dc_u4 va, vb, vc, vd;
-        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %5\n\tds_read_b128 %2, %6\n\tds_read_b128 %3, %7\n\t"
-                     "s_waitcnt lgkmcnt(0)"
-                     : "=&v"(va), "=&v"(vb), "=&v"(vc), "=&v"(vd)
-                     : "v"(dc_lds_addr(ssm + ((r0 + c0) * 4 + cd) * 8)), "v"(dc_lds_addr(ssm + ((r0 + c1) * 4 + cd) * 8)),
-                       "v"(dc_lds_addr(ssm + ((r1 + c0) * 4 + cd) * 8)), "v"(dc_lds_addr(ssm + ((r1 + c1) * 4 + cd) * 8))
-                     : "memory");
-        const uint4 a = __builtin_bit_cast(uint4, va), b = __builtin_bit_cast(uint4, vb);
-        const uint4 c = __builtin_bit_cast(uint4, vc), d = __builtin_bit_cast(uint4, vd);
+        const uint4 a = *reinterpret_cast<const uint4*>(ssm + ((r0 + c0) * 4 + cd) * 8);
+        const uint4 b = *reinterpret_cast<const uint4*>(ssm + ((r0 + c1) * 4 + cd) * 8);
+        const uint4 c = *reinterpret_cast<const uint4*>(ssm + ((r1 + c0) * 4 + cd) * 8);
+        const uint4 d = *reinterpret_cast<const uint4*>(ssm + ((r1 + c1) * 4 + cd) * 8);
         const uint4 v = bilerp8_mix(a, b, c, d, wx, wy);
         const uint4 o = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-        asm volatile("ds_write_b128 %0, %1" ::"v"(dc_lds_addr(psm + (u & 1) * DC_PSLOT + sl * 8)),
-                     "v"(__builtin_bit_cast(dc_u4, o))
-                     : "memory");
+        *reinterpret_cast<uint4*>(psm + (u & 1) * DC_PSLOT + sl * 8) = o;
       }
     }
   };
