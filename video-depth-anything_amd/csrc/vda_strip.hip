@@ -38,6 +38,11 @@ constexpr int ST_PPW = (ST_PP + 7) / 8;                     // per wave, fixed (
 constexpr int ST_PBUF = ST_PPW * 8 * 512;                   // halfs per patch ring slot (56 KiB)
 constexpr int ST_N = 256;                                   // output channels
 constexpr int ST_WBUF = ST_N * ST_CPX * 8;                  // halfs per weight step (16 KiB)
+#ifdef ST_W2
+constexpr int ST_WR = 2;                                    // weight ring slots (A/B: the round-1 ring)
+#else
+constexpr int ST_WR = 3;                                    // weight ring: step t+2's weights in flight
+#endif
 
 struct StripParams {
   const h16* x;
@@ -65,7 +70,7 @@ __device__ __forceinline__ int st_ppos(int pp, int cd) { return cd ^ ((pp >> 1) 
 __device__ __forceinline__ int st_wpos(int n, int cd) { return cd ^ ((n >> 1) & 3); }
 
 __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
-  __shared__ __attribute__((aligned(16))) h16 sm[2 * ST_PBUF + 2 * ST_WBUF];
+  __shared__ __attribute__((aligned(16))) h16 sm[2 * ST_PBUF + ST_WR * ST_WBUF];  // 160 KiB with 3 slots
   h16* patch = sm;
   h16* wbuf = sm + 2 * ST_PBUF;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -121,13 +126,18 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
       const int s = piece * 64 + lane;
       const int n = s / ST_CPX, pos = s - n * ST_CPX;
       const int cd = st_wpos(n, pos);
-      st_glds16(p.w + (long)n * K + tap * p.Cin + slab * ST_SLAB + cd * 8, wbuf + (gs & 1) * ST_WBUF + piece * 512);
+      st_glds16(p.w + (long)n * K + tap * p.Cin + slab * ST_SLAB + cd * 8, wbuf + (gs % ST_WR) * ST_WBUF + piece * 512);
     }
   };
 
   for (int j = 0; j < ST_PPW; ++j) dma_patch(0, j);
   dma_w(0);
-  st_wait<0>();
+  if (ST_WR == 3 && my_steps > 1) {
+    dma_w(1);
+    st_wait<2>();
+  } else {
+    st_wait<0>();
+  }
   __builtin_amdgcn_s_barrier();
 
   const int frow = lane & 15, g = lane >> 4;
@@ -141,7 +151,9 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
 
   for (int gs = 0; gs < my_steps; ++gs) {
     const int u = gs / 9, tap = gs - u * 9;
-    if (gs + 1 < my_steps) dma_w(gs + 1);
+    const int wahead = gs + ST_WR - 1;                 // the step whose weights are issued now
+    const bool issue_w = wahead < my_steps;
+    if (issue_w) dma_w(wahead);
     const bool issue_p = tap == 0 && u + 1 < my_units;
     if (issue_p)
       for (int j = 0; j < ST_PPW; ++j) dma_patch(u + 1, j);
@@ -161,7 +173,7 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
     const int dy = tap / 3, dx = tap - dy * 3;
     const int toff = (dy - 1) * PW + (dx - 1);
     const h16* pb = patch + (u & 1) * ST_PBUF;
-    const h16* wb = wbuf + (gs & 1) * ST_WBUF;
+    const h16* wb = wbuf + (gs % ST_WR) * ST_WBUF;
     {
       const int cd = g;
       h8 xf[4];
@@ -218,9 +230,27 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
           }
         }
       }
+      // compiler-visible vmcnt(0) once per work item: without it the loads / stores above stay
+      // "pending" across the loop back-edge and hipcc put an s_waitcnt vmcnt(0) before the first VGPR
+      // write of every step (draining the weight ring)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
     }
-    if (issue_p) st_wait<ST_PPW>();
-    else st_wait<0>();
+    if constexpr (ST_WR == 2) {
+      if (issue_p) st_wait<ST_PPW>();
+      else st_wait<0>();
+    } else {
+      // step gs + 1's weights must have landed; newer than them: this step's weights (2 pieces) and
+      // the next unit's patch pieces when issued this step (after the weights) or the previous step
+      // (tap 1: before this step's weights; they then land by the end of tap 1, 8 steps early)
+      const bool p_prev = tap == 1 && u + 1 < my_units;
+      if (issue_w) {
+        if (issue_p || p_prev) st_wait<ST_PPW + 2>();
+        else st_wait<2>();
+      } else {
+        if (issue_p || p_prev) st_wait<ST_PPW>();
+        else st_wait<0>();
+      }
+    }
     __builtin_amdgcn_s_barrier();
   }
 }
