@@ -2,6 +2,7 @@
 
 usage: python tools/ab_conv.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes oc1,depth,rcu148]
 oc1:    output_conv1, 3x3 256 -> 128 on the x2 bilinear resize of a [32, 148, 148, 256] map (fused)
+oc1u:   the same through the materialised resize + the plain halo conv (compare with oc1: same output)
 depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
 rcu148: refinenet1 RCU conv, 3x3 256 -> 256 at 148^2 with pre-ReLU + ReLU
 l3rn / l4rn: layer3_rn / layer4_rn, 3x3 1024 -> 256 (no bias) at 37^2 / 19^2 (the strip conv; 19^2 splits)
@@ -47,6 +48,20 @@ def case(name):
             return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 128, 3, 1, 1, 0, 296, 296,
                                 ctypes.byref(e), None, 0, st)
         return run, y, fl, [x, w, b, e]
+    if name == "oc1u":  # the unfused route: the x2 resize materialised, then the plain halo conv at 296^2
+        x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
+        u = torch.empty(32, 296, 296, 256, device=dev, dtype=torch.float16)
+        w = (torch.randn(128, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
+        b = torch.randn(128, device=dev) * 0.1
+        y = torch.empty(32, 296, 296, 128, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1, bias=b.data_ptr())
+        fl = 2.0 * 32 * 296 * 296 * 128 * 2304
+
+        def run(l):
+            rc = l.vda_upsample_bilinear(x.data_ptr(), u.data_ptr(), 32, 148, 148, 256, 296, 296, st)
+            return rc or l.vda_conv2d(u.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 296, 296, 256, 128, 3, 1, 1, 0, 0, 0,
+                                      ctypes.byref(e), None, 0, st)
+        return run, y, fl, [x, u, w, b, e]
     if name == "rcu148":
         x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
         w = (torch.randn(256, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()

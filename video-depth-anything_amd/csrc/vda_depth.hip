@@ -24,6 +24,9 @@
 namespace {
 
 __device__ __attribute__((aligned(64))) uint4 g_dz_page[4];
+#ifdef VDA_TS  // per-block step-class cycle sums of output_conv1 (tools/ts_oc1.py; experiments only)
+__device__ unsigned long long g_dts[1024][24];
+#endif
 
 constexpr int DT = 16;              // output tile edge
 constexpr int DP = DT + 2;          // patch edge (halo 1)
@@ -265,6 +268,16 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
 
   // step counters kept incrementally (no per-step division): unit u, its step st and slab
   int u = 0, st = 0, slab = 0;
+#ifdef VDA_TS
+  // class = step within the unit (0..SPU-1), SPU = a tile's last step; sums of s_memtime deltas between
+  // consecutive end-of-step barriers (and of the end-of-step wait + barrier alone), taken by every wave
+  // (uniform), stored by thread 0 at the end
+  unsigned long long tsa[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned tsn[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const unsigned long long ts_rt0 = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long ts_c0 = __builtin_amdgcn_s_memtime();
+  unsigned long long ts_prev = ts_c0, tsw = 0;
+#endif
   for (int gs = 0; gs < my_steps; ++gs) {
     // weights of the next step first, then (first step of a unit) the whole next patch slab: the
     // end-of-step wait then leaves exactly the patch pieces in flight, and they land by the end of
@@ -386,6 +399,9 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       }
       tile_of_unit(u, pend_bt, pend_y0, pend_x0);
     }
+#ifdef VDA_TS
+    const unsigned long long ts_pre = __builtin_amdgcn_s_memtime();
+#endif
     if constexpr (UPS) {
       if (issue_p) dh_wait_vmcnt<SPPW>();
       else dh_wait_vmcnt<0>();
@@ -396,6 +412,17 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       dh_wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
+#ifdef VDA_TS
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+      const int cls = tile_end ? SPU : st;
+#pragma unroll
+      for (int c = 0; c <= SPU && c < 10; ++c)
+        if (c == cls) { tsa[c] += now - ts_prev; ++tsn[c]; }
+      tsw += now - ts_pre;
+      ts_prev = now;
+    }
+#endif
     if (DEPTH && tile_end) {
       if (ng == 0 && lane < 16) {
         const float bias2 = b2[0];
@@ -413,9 +440,24 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       if (++slab == nslab) slab = 0;
     }
   }
+#ifdef VDA_TS
+  if (!DEPTH && UPS && tid == 0 && blockIdx.x < 1024) {
+    const unsigned long long rt = __builtin_amdgcn_s_memrealtime() - ts_rt0, cy = __builtin_amdgcn_s_memtime() - ts_c0;
+    for (int c = 0; c < 10; ++c) { g_dts[blockIdx.x][c] = tsa[c]; g_dts[blockIdx.x][10 + c] = tsn[c]; }
+    g_dts[blockIdx.x][20] = rt;
+    g_dts[blockIdx.x][21] = cy;
+    g_dts[blockIdx.x][22] = tsw;
+  }
+#endif
 }
 
 }  // namespace
+
+#ifdef VDA_TS
+extern "C" int vda_debug_oc1_timestamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dts), sizeof(g_dts), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // called by vda_depth_head (vda_gemm.hip) after the resize into ws; returns 1 if the shape is not
 // supported here (caller falls back to the implicit-GEMM kernel)
