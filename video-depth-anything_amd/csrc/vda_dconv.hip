@@ -65,6 +65,9 @@ __device__ __forceinline__ void dc_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F);
 // formula: bit-identical to resize + conv) by the block's own waves after their MFMAs of the unit's
 // middle row, while the other block of the CU keeps the matrix cores busy.  W then uses a 2-slot ring
 // (one phase ahead) to make room for the 12-KiB source slot.
+#ifdef VDA_TS  // per-block phase-class cycle sums of the fused depth conv (tools/ts_dconv.py; experiments only)
+__device__ unsigned long long g_dcts[1024][12];
+#endif
 template <bool UPS>
 __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
                                                            const float* __restrict__ b1, const float* __restrict__ w2,
@@ -288,8 +291,26 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
       for (int m = 0; m < 4; ++m) acc[n][m] = mfma16(wf[n], xf[m], acc[n][m]);
   };
 
+#ifdef VDA_TS
+  // class of the phase that just ended: its row dy (0..2), 3 = a tile's last phase (with the epilogue);
+  // sums of s_memtime deltas between phase-start barriers, and of the end-of-phase wait + barrier alone
+  unsigned long long tsa[4] = {0, 0, 0, 0}, tsn[4] = {0, 0, 0, 0}, tsw = 0;
+  const unsigned long long ts_rt0 = __builtin_amdgcn_s_memrealtime(), ts_c0 = __builtin_amdgcn_s_memtime();
+  unsigned long long ts_prev = ts_c0, ts_pre = ts_c0;
+  int ts_cls = -1;
+#endif
   auto phase = [&](int g, int u, int dy) {
     __builtin_amdgcn_s_barrier();
+#ifdef VDA_TS
+    {
+      const unsigned long long now = __builtin_amdgcn_s_memtime();
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c == ts_cls) { tsa[c] += now - ts_prev; ++tsn[c]; }
+      if (ts_cls >= 0) tsw += now - ts_pre;
+      ts_prev = now;
+    }
+#endif
     // after barrier g every wave is done with phase g - 1's reads: refill its W slot, and (first
     // phase of a unit) the patch slot unit u - 1 read
     const bool wnext = g + (UPS ? 1 : 2) < G;
@@ -346,6 +367,9 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
         for (int n = 0; n < 4; ++n) acc[n][m] = f4{0.f, 0.f, 0.f, 0.f};
       }
     }
+#ifdef VDA_TS
+    ts_cls = (dy == 2 && (u % nslab) == nslab - 1) ? 3 : dy;
+#endif
     if constexpr (UPS) {
       // row 1: this unit's MFMAs are issued; build the next unit's patch (its source region arrived
       // by the row-0 wait), writes complete before barrier g + 1 (a 3 + 3 split over rows 1 and 2,
@@ -356,6 +380,9 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
       }
       // W(g + 1) (issued this phase) must have landed before barrier g + 1; so must, at row 0, the
       // source region of unit u + 1 (issued in row 2 of unit u - 1).  Newer: row 2's source pieces
+#ifdef VDA_TS
+      ts_pre = __builtin_amdgcn_s_memtime();
+#endif
       dc_wait_n(dy == 2 && u + 2 < my_units ? 3 : 0);
     } else {
       // W(g + 1) (issued in phase g - 1) and, at a unit's last row, the next unit's patch (issued in its
@@ -365,9 +392,23 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
     }
    }
   }
+#ifdef VDA_TS
+  if (UPS && threadIdx.x == 0 && blockIdx.x < 1024) {
+    for (int c = 0; c < 4; ++c) { g_dcts[blockIdx.x][c] = tsa[c]; g_dcts[blockIdx.x][4 + c] = tsn[c]; }
+    g_dcts[blockIdx.x][8] = __builtin_amdgcn_s_memrealtime() - ts_rt0;
+    g_dcts[blockIdx.x][9] = __builtin_amdgcn_s_memtime() - ts_c0;
+    g_dcts[blockIdx.x][10] = tsw;
+  }
+#endif
 }
 
 }  // namespace
+
+#ifdef VDA_TS
+extern "C" int vda_debug_dconv_timestamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dcts), sizeof(g_dcts), 0, hipMemcpyDeviceToHost);
+}
+#endif
 
 // vda_debug_dconv (tuning build): -1 automatic (fused), 0 never, 2 resize + unfused depth conv
 VDA_KNOB(int, g_dconv_mode, -1);
