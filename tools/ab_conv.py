@@ -5,6 +5,7 @@ oc1:    output_conv1, 3x3 256 -> 128 on the x2 bilinear resize of a [32, 148, 14
 oc1u:   the same through the materialised resize + the plain halo conv (compare with oc1: same output)
 depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
 rcu148: refinenet1 RCU conv, 3x3 256 -> 256 at 148^2 with pre-ReLU + ReLU
+rcu148r: the RCU's second conv (pre-ReLU, bias, + residual)
 l3rn / l4rn: layer3_rn / layer4_rn, 3x3 1024 -> 256 (no bias) at 37^2 / 19^2 (the strip conv; 19^2 splits)
 Outputs compared bit-for-bit against the first library's.
 """
@@ -62,6 +63,20 @@ def case(name):
             return rc or l.vda_conv2d(u.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 296, 296, 256, 128, 3, 1, 1, 0, 0, 0,
                                       ctypes.byref(e), None, 0, st)
         return run, y, fl, [x, u, w, b, e]
+    if name == "rcu148r":  # the RCU's second conv: pre-ReLU, bias, + the block input as residual
+        x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
+        w = (torch.randn(256, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
+        b = torch.randn(256, device=dev) * 0.1
+        r = torch.randn(32, 148, 148, 256, device=dev).half()
+        y = torch.empty(32, 148, 148, 256, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1, bias=b.data_ptr())
+        e.res = r.data_ptr(); e.ldres = 256
+        fl = 2.0 * 32 * 148 * 148 * 256 * 2304
+
+        def run(l):
+            return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 256, 3, 1, 1, 1, 0, 0,
+                                ctypes.byref(e), None, 0, st)
+        return run, y, fl, [x, w, b, r, e]
     if name == "rcu148":
         x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
         w = (torch.randn(256, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
