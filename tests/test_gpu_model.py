@@ -89,3 +89,18 @@ def test_bn_clstoken_variant_matches_reference_golden(fp32):
     err = rel_l1(d, depth)
     print(f"bn+clstoken fp32={fp32}: rel-L1 vs reference = {err:.3e}")
     assert err <= (1e-5 if fp32 else TOL_FP16)
+
+
+def test_forward_input_checks_mirror_reference_asserts():
+    """The reference's shape asserts at the boundary: H, W multiples of 14 (patch_embed.py:73-74),
+    T <= the temporal PE table (motion_module.py:198-206), 3 input channels (patch_embed.py:69)."""
+    m = model("vits")
+    with pytest.raises(AssertionError, match="multiple of the patch size"):
+        m(torch.zeros(1, 2, 3, 70, 99, device="cuda"))
+    with pytest.raises(ValueError, match="exceeds the temporal PE table"):
+        m(torch.zeros(1, 33, 3, 28, 28, device="cuda"))
+    with pytest.raises(ValueError, match="3 input channels"):
+        m(torch.zeros(1, 2, 4, 28, 28, device="cuda"))
+    # T = 1 (a single frame through the temporal blocks) is valid
+    d = m(torch.randn(1, 1, 3, 28, 42, device="cuda"))
+    assert d.shape == (1, 1, 28, 42) and torch.isfinite(d).all()
