@@ -370,7 +370,10 @@ __global__ __launch_bounds__(256) void gemm_reg_kernel(GemmParams p, int tiles_n
 // GROUP_M m-panels at a time so co-resident blocks share X panels and W tiles in their XCD's L2.
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
-constexpr int GROUP_M = 8;
+#ifndef VDA_GROUP_M
+#define VDA_GROUP_M 8
+#endif
+constexpr int GROUP_M = VDA_GROUP_M;  // m-panels per XCD tile group (tuning: -DVDA_GROUP_M=...)
 constexpr int ACT_DEPTH = 4;  // internal: depth-head tail epilogue (vda_depth_head)
 
 __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
