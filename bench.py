@@ -27,8 +27,10 @@ Extra fields:
                 single-stream forwards right after it, see roofline.probe); achieved = algorithmic FLOPs per launch / mean
                 launch time vs 2.5 PFLOP/s dense fp16; traffic from profiles/<round>_pmc_fc1.json
                 (rocprofv3 PMC, gfx950-corrected), mfma_busy_pmc from profiles/<round>_pmc_mfma.json
-  cpu_baseline  the oracle's fp32 PyTorch-CPU forward (oracle/vda_oracle.py) of one full clip of the
-                same workload (default: all 32 frames), rank 0 / N=1 only - a reported baseline only.
+  cpu_baseline  the oracle's fp32 PyTorch-CPU forward (oracle/vda_oracle.py) of one whole clip of the
+                same workload (default all 32 frames, ~80 s on 16 threads; ``--cpu-baseline-frames F``
+                times a 1xF clip instead, recorded in ``frames``), rank 0 / N=1 only - a reported
+                baseline only.
 """
 from __future__ import annotations
 
@@ -62,9 +64,9 @@ def parse():
     ap.add_argument("--clips-per-gpu", type=int, default=1)
     ap.add_argument("--video", action="store_true", help="time infer_video_depth on a synthetic video (configs[3])")
     ap.add_argument("--video-frames", type=int, default=176, help="frames of the --video input (176 = 8 windows)")
-    ap.add_argument("--cpu-baseline-frames", type=int, default=8,
-                    help="frames of the CPU-oracle clip timed as the cpu_baseline (0 disables; the default 8 is "
-                         "a bounded ~20-s sample of the 32-frame workload, the same model at the same frame size)")
+    ap.add_argument("--cpu-baseline-frames", type=int, default=32,
+                    help="frames of the CPU-oracle clip timed as the cpu_baseline (0 disables; the default is the "
+                         "whole 32-frame clip of the workload, ~80 s on the box's 16 threads)")
     ap.add_argument("--no-probe", action="store_true", help="skip the per-launch event probe")
     ap.add_argument("--graph", action="store_true", help="replay the forward as a captured HIP graph")
     ap.add_argument("--streams", type=int, default=2,
@@ -380,7 +382,7 @@ def cpu_baseline(model, x, enc, nframes, H, W):
     vda_oracle.forward(sd, enc, xs)
     cpu_s = time.perf_counter() - t1
     return {"value": round(xs.shape[1] / cpu_s, 4), "unit": "frames/s", "cores": torch.get_num_threads(),
-            "kind": "port", "cpu": cpu_model(),
+            "kind": "port", "cpu": cpu_model(), "frames": int(xs.shape[1]),
             "sample": f"oracle fp32 PyTorch-CPU forward of one {enc} 1x{xs.shape[1]}x3x{H}x{W} clip "
                       f"({cpu_s:.1f} s, {torch.get_num_threads()} threads)"}
 

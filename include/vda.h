@@ -73,7 +73,8 @@ typedef struct vda_epilogue {
   /* ln_parts > 0: ln_stats instead holds [M, ln_parts, 2] partial (sum, sum of squares) of row m
    * over ln_parts column blocks (as written through stats_out by the GEMM that produced X); the
    * epilogue forms mean = sum / K, var = max(sumsq / K - mean^2, 0), rstd = 1 / sqrt(var + ln_eps).
-   * ln_parts <= 4.  No padding is needed past [M, ln_parts, 2]: the kernels never read beyond it. */
+   * ln_parts <= 4, M * max(ln_parts, 1) >= 2.  No padding is needed past [M, ln_parts, 2]: the kernels
+   * never read beyond it. */
   int32_t ln_parts;
   float ln_eps;
   /* Producer side: write [M, ceil(N / 256), 2] per-row partial (sum, sum of squares) of the fp16

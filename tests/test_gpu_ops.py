@@ -800,3 +800,52 @@ def test_gemm_layernorm_fold_odd_stats_exact_size(M, P, rowbias, nobias):
     err_last = rel(y[-1:], ref[-1:])
     print(f"LN fold odd stats M={M} P={P} rowbias={rowbias}: rel-L1 {err:.2e}, last row {err_last:.2e}")
     assert err < 3e-3 and err_last < 5e-3
+
+
+@pytest.mark.parametrize("kind", ["offset", "outlier_channels"])
+@pytest.mark.parametrize("N2,act", [(3072, 0), (4096, ACT_GELU)])
+def test_gemm_layernorm_fold_stress_statistics(kind, N2, act):
+    """the LN fold's numerics on activation statistics like a trained DINOv2-L's
+    (block.py:84,87; the reference's autocast LayerNorm runs in fp32).  The residual stream goes through
+    the producer GEMM (proj / fc2: x += ..., stats_out partials over 256-column blocks) and then the
+    LN-folded consumer (qkv / fc1) reads those partials; compared with torch fp32 LayerNorm -> Linear on
+    the same stored fp16 residual values.  Rows carry either a common offset of 50-100 sigma (the
+    E[x^2] - mean^2 cancellation) or a few channels at ~500 (DINOv2's massive activations)."""
+    M, C, Kp = 8192, 1024, 1024
+    g = torch.Generator().manual_seed(N2 + (1 if kind == "offset" else 2))
+    if kind == "offset":
+        sig = 0.5 + torch.rand(M, 1, generator=g)
+        mu = (50 + 50 * torch.rand(M, 1, generator=g)) * sig * torch.sign(torch.randn(M, 1, generator=g))
+        r = torch.randn(M, C, generator=g) * sig + mu
+    else:
+        r = torch.randn(M, C, generator=g)
+        hot = torch.randint(0, C, (4,), generator=g)
+        r[:, hot] = 400 + 200 * torch.rand(M, 4, generator=g)
+    r = r.half()
+    x = (torch.randn(M, Kp, generator=g) * 0.5).half()
+    w = torch.randn(C, Kp, generator=g) * Kp ** -0.5 * 0.1
+    b = 0.01 * torch.randn(C, generator=g)
+    P = C // 256
+    tok = r.to(DEV).contiguous()
+    st = torch.empty(M, P, 2, device=DEV)
+    ops.gemm(h(x.float()), h(w), bias=f32(b), res=tok, out=tok, stats_out=st)
+    y = tok.float().cpu()  # the stored residual stream the consumer normalises
+    gam, bet = 1 + 0.2 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    w2 = torch.randn(N2, C, generator=g) * C ** -0.5
+    b2 = 0.1 * torch.randn(N2, generator=g)
+    wg = (w2 * gam[None, :]).half()
+    c1, bb = f32(wg.float().sum(1)), f32(w2 @ bet + b2)
+    ya = ops.gemm(tok, wg.to(DEV), bias=bb, act=act, ln_stats=st, ln_parts=P, ln_eps=1e-6, ln_colsum=c1)
+    ref = F.linear(F.layer_norm(y, (C,), gam, bet, eps=1e-6), w2, b2)
+    if act == ACT_GELU:
+        ref = F.gelu(ref)
+    # the per-row (mean, rstd) the partials imply, vs fp64 statistics of the stored values
+    s = st.double().cpu().sum(1)
+    mean = s[:, 0] / C
+    rstd = ((s[:, 1] / C - mean * mean).clamp_min(0) + 1e-6).rsqrt()
+    yd = y.double()
+    rstd_ref = (yd.var(1, unbiased=False) + 1e-6).rsqrt()
+    rstd_err = ((rstd - rstd_ref).abs() / rstd_ref).max().item()
+    err = rel(ya, ref)
+    print(f"LN fold stress {kind} N={N2} act={act}: rel-L1 {err:.2e}, max rstd rel err {rstd_err:.2e}")
+    assert err < 1e-3

@@ -349,19 +349,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
     h8 pf[4];
     float t0, t1;
     auto expo = [&]() {
-#ifdef SA_TREE  // experiment: four interleaved partial sums (shorter add chains)
-      float u[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
-          u[kb * 2 + (r & 1)] += pv;
-          pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
-        }
-      t0 = u[0] + u[1];
-      t1 = u[2] + u[3];
-#else
       t0 = 0.f;
       t1 = 0.f;
 #pragma unroll
@@ -373,7 +360,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
           else t1 += pv;
           pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
         }
-#endif
     };
     if constexpr (FIRST) {
       rebase(tile_max());
@@ -470,9 +456,7 @@ __device__ __forceinline__ void rope_frag(h8& q, h8& k, int t, int c0, int C, fl
 
 __device__ __attribute__((aligned(64))) uint4 g_ta_zero[4];
 
-#ifndef VDA_TA_NW
-#define VDA_TA_NW 4  // waves (heads of one site) per temporal-attention block
-#endif
+constexpr int VDA_TA_NW = 4;  // waves (heads of one site) per temporal-attention block
 template <int DP>
 __global__ __launch_bounds__(64 * VDA_TA_NW) void temporal_attn_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
                                                             int B, int T, int S, int H, int D, float scale_log2,

@@ -21,12 +21,7 @@ typedef float f16x __attribute__((ext_vector_type(16)));
 #define VDA_LDS __attribute__((address_space(3)))
 
 __device__ __forceinline__ f4 mfma16(h8 a, h8 b, f4 c) {
-#ifdef VDA_MFMA_BF16  // power/clock experiments only (tools/bf16_probe.py)
-  typedef __bf16 b8 __attribute__((ext_vector_type(8)));
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
-#else
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-#endif
 }
 __device__ __forceinline__ f16x mfma32(h8 a, h8 b, f16x c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);

@@ -32,9 +32,7 @@ extern "C" int vda_debug_timestamps(void* host) {
 // cache policy of the phased epilogue's output stores: nt (aux = 2).  In-situ A/B on one box
 // (tools/ab_libs.sh, 2 rounds): every phased GEMM/conv class 0.7-3.6 % faster, the forward's kernel
 // sum 55.77 -> 55.33 ms; the output tile is not re-read by the launch, so it need not stay in L2.
-#ifndef VDA_EPI_STORE_AUX
-#define VDA_EPI_STORE_AUX 2
-#endif
+constexpr int VDA_EPI_STORE_AUX = 2;
 
 // halo-tiled 3x3 kernels (vda_depth.hip)
 int vda_depth_halo(const void* U, const void* w1, const float* b1, const float* w2, const float* b2, float* depth,
@@ -370,10 +368,7 @@ __global__ __launch_bounds__(256) void gemm_reg_kernel(GemmParams p, int tiles_n
 // GROUP_M m-panels at a time so co-resident blocks share X panels and W tiles in their XCD's L2.
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
-#ifndef VDA_GROUP_M
-#define VDA_GROUP_M 8
-#endif
-constexpr int GROUP_M = VDA_GROUP_M;  // m-panels per XCD tile group (tuning: -DVDA_GROUP_M=...)
+constexpr int GROUP_M = 8;  // m-panels per XCD tile group (2 / 4 / 16 within noise: profiles/r04_ab_gemm_group_m.log)
 constexpr int ACT_DEPTH = 4;  // internal: depth-head tail epilogue (vda_depth_head)
 
 __device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
@@ -417,7 +412,8 @@ __device__ __forceinline__ float2 lds_ld_f2(const float* ptr) {
   return v;
 }
 __device__ __forceinline__ void lds_ld_f4x2(const float* ptr, float4& a, float4& b) {
-  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)" : "=v"(a), "=v"(b)
+  // early-clobber outputs: the second read must not take its address from the first read's destination
+  asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)" : "=&v"(a), "=&v"(b)
                : "v"((unsigned)(uintptr_t)(VDA_LDS const float*)ptr) : "memory");
 }
 __device__ __forceinline__ float lds_ld_f1(const float* ptr) {
@@ -1693,11 +1689,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, false, -1, wave);
     TS(7);
   } else {
-    // row-store epilogues chain the next tile's prologue (gemm256_tile); the scatter store does not
-#ifndef VDA_CHAIN_STAGED  // chain the staged row-store epilogue too: measured 4 % slower on proj (106.0
-#define VDA_CHAIN_STAGED 0  // -> 110.3 us, same box), fc2 unchanged; the register epilogues always chain
-#endif
-    const bool chain = EK ? true : (VDA_CHAIN_STAGED && p.epi.store == VDA_STORE_ROWS);
+    // the fixed-kind epilogues chain the next tile's prologue (gemm256_tile); the generic (EK 0) one
+    // does not (chaining the staged row store measured 4 % slower on proj, 106.0 -> 110.3 us, round 3)
+    const bool chain = EK != 0;
     bool pre = false;
     for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
       TS(0);
@@ -1721,10 +1715,7 @@ VDA_KNOB(int, g_desync, 0);       // vda_debug_gemm_desync
 // 104.9 -> 111.9, fc2 319.2 -> 331.2, same box, tools/ab_gemm.py, profiles/r04_ab_gemm_ek2.log): the
 // residual loads issued at the epilogue start are waited for right away, where the staged epilogue
 // covers them with its LDS staging pass.
-#ifndef VDA_RES_EPI_DEFAULT
-#define VDA_RES_EPI_DEFAULT 0
-#endif
-VDA_KNOB(int, g_res_epi, VDA_RES_EPI_DEFAULT);
+VDA_KNOB(int, g_res_epi, 0);
 
 int cu_count() { return vda_cu_count(); }
 
@@ -1734,12 +1725,6 @@ void phased_sched(int ntiles, int nk, bool conv, int& grid, int& ticks) {
   // measured in situ: persistent pays for the dense GEMMs, one block per tile for the convs
   const int persist = conv ? 0 : (g_persist >= 0 ? g_persist : cus);
   grid = persist == 0 ? ntiles : std::min(ntiles, persist);
-#ifdef VDA_RIGHTSIZE  // experiment: the fewest blocks that keep the round count (the rest of the CUs stay free)
-  if (persist > 0 && ntiles > grid) {
-    const int rounds = (ntiles + grid - 1) / grid;
-    grid = (ntiles + rounds - 1) / rounds;
-  }
-#endif
   // The start stagger for a short last round (half the blocks with one tile fewer start half a
   // tile late, ~1.45 us per 64-deep K step + ~6 us prologue/epilogue) is off by default: it is worth
   // +0.4 % with one clip in flight but -0.6 % with the two clips in flight the drivers run (the
@@ -1899,7 +1884,7 @@ vda_epilogue default_epi() {
   return e;
 }
 
-int check_epi(const vda_epilogue& e, int N) {
+int check_epi(const vda_epilogue& e, int M, int N) {
   VDA_CHECK_ARG(!e.rowbias || (e.rdiv > 0 && e.rmod > 0), "rowbias needs rdiv, rmod > 0");
   VDA_CHECK_ARG(e.act >= 0 && e.act <= 3, "unknown activation");
   VDA_CHECK_ARG(e.act != VDA_ACT_GEGLU || (N % 32 == 0 && !e.rowbias && e.store == 0 && !e.res2),
@@ -1918,6 +1903,9 @@ int check_epi(const vda_epilogue& e, int N) {
                     (e.act == VDA_ACT_NONE && e.bias && !e.res && !e.res2 && !e.stats_out && e.rdiv >= 256),
                 "ln_stats with rowbias needs a bias, no activation / residual / stats_out, rdiv >= 256");
   VDA_CHECK_ARG(!e.ln_stats || (e.ln_parts >= 0 && e.ln_parts <= 4), "ln_parts must be 0 .. 4");
+  // the phased route stages the statistics in 16-byte pieces, reading the last one 8 B early when the
+  // float count is not a multiple of 4: the buffer must hold at least one whole piece (M * P >= 2)
+  VDA_CHECK_ARG(!e.ln_stats || (long)M * (e.ln_parts > 0 ? e.ln_parts : 1) >= 2, "ln_stats needs M * max(ln_parts, 1) >= 2");
   VDA_CHECK_ARG(!e.stats_out || (e.store == VDA_STORE_ROWS && e.act != VDA_ACT_GEGLU),
                 "stats_out needs a row store and no GEGLU");
   VDA_CHECK_ARG(!e.res || e.ldres % 4 == 0, "ldres % 4");
@@ -1940,7 +1928,7 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
   VDA_CHECK_ARG(p.epi.res2_h == 0 && p.epi.res2_w == 0, "upsampled res2: vda_conv2d only");
-  int rc = check_epi(p.epi, N);
+  int rc = check_epi(p.epi, M, N);
   if (rc) return rc;
   if (p.epi.ln_stats && p.epi.rowbias) {  // only the phased 256x256 route (EK 3) implements the pair
     const bool a16 = ((uintptr_t)p.y % 16 == 0) && ldy % 8 == 0 && ((uintptr_t)p.x % 16 == 0);
@@ -2005,7 +1993,7 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
   VDA_CHECK_ARG(p.epi.store == VDA_STORE_ROWS && (p.epi.act == VDA_ACT_NONE || p.epi.act == VDA_ACT_RELU),
                 "conv: row store, activation none/relu");
   VDA_CHECK_ARG(!p.epi.stats_out && !p.epi.ln_stats, "conv: no LayerNorm fold / row statistics");
-  int rc = check_epi(p.epi, Cout);
+  int rc = check_epi(p.epi, p.M, Cout);
   if (rc) return rc;
   const bool res2_up = p.epi.res2_h > 0 || p.epi.res2_w > 0;
   if (res2_up) {  // refinenet1's skip add on the previous block's output, upsampled in the epilogue

@@ -42,7 +42,8 @@ constexpr int HC_NPIX = (HC_TR + 2) * HC_PC;         // 340 patch pixels
 constexpr int HC_PSTR = 9;                           // 16-B slots per patch pixel (8 channel chunks + 1 pad)
 constexpr int HC_PP = (HC_NPIX * HC_PSTR + 63) / 64; // 48 one-KiB DMA pieces per 64-channel slab
 constexpr int HC_PSLOT = HC_PP * 512;                // halfs per patch slot
-constexpr int HC_PPW = (HC_PP + 7) / 8;              // patch pieces per wave (6; waves 3-7 own 5)
+constexpr int HC_PPW = (HC_PP + 7) / 8;              // patch pieces per wave: every wave owns exactly 6
+static_assert(HC_PP % 8 == 0, "the hc_wait counts assume every wave issues HC_PPW patch pieces");
 constexpr int HC_BK = 64;
 constexpr int HC_HALF = 128 * HC_BK;                 // halfs per 128-row W region
 constexpr int HC_WBUF = 2 * HC_HALF;                 // one K step of W (256 rows)
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
 
   // the 9 taps of a slab unrolled: tap offsets, patch-piece and relu-pass slots are compile-time (the
   // rolled loop's per-step tap / slab division and the run-time piece select cost 824 -> 717 us on
-  // refinenet1's RCU conv, bit-identical; profiles/r04_ab_hconv.log).  Per step, 4 phases:
+  // refinenet1's RCU conv, bit-identical; profiles/r04_ab_hconv_unroll.log).  Per step, 4 phases:
   // P1 (+ one piece of the next slab's patch in steps 0..HC_PPW-1), P2 (+ the next step's W quarter,
   // the relu pass of the next slab in steps 7 / 8), P3, P4 (retire everything but this phase's W(t+2))
   for (int slab = 0; slab < nslab; ++slab) {
@@ -299,7 +300,6 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   HTS(2);
   __syncthreads();
 
-#ifndef HC_EPI_LATE_PREFETCH
   // residual / upsampled-res2 prefetch issued before the LDS staging pass below, so its latency runs
   // under the staging instead of in front of the first store
   // thread -> 16-B chunk q of pixels row0 + 16 it (it = 0..15): tile row it >> 1, column row0 + 16 (it & 1)
@@ -359,7 +359,6 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
 #pragma unroll
     for (int it = 0; it < PD; ++it) q2[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, voff(it), 0, 0));
   }
-#endif
   // ---- epilogue: +bias [ReLU] -> fp16 [256 px][256 ch] image in LDS (8-byte units XOR-swizzled by
   // pixel & 15), then whole 512-B pixel rows + residuals -> global
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
@@ -385,65 +384,6 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
   }
   __syncthreads();
   HTS(3);
-#ifdef HC_EPI_LATE_PREFETCH
-  // thread -> 16-B chunk q of pixels row0 + 16 it (it = 0..15): tile row it >> 1, column row0 + 16 (it & 1)
-  const int q = tid & 31, row0 = tid >> 5;
-  const h16* l0 = smem + row0 * 256 + ((2 * q) ^ row0) * 4;
-  const h16* l1 = smem + row0 * 256 + ((2 * q + 1) ^ row0) * 4;
-  const long fbytes = (long)H * W * 512;
-  const long fbase = (long)bt * H * W * 256;
-  auto rsrc = [&](const h16* p) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + fbase), (short)0, (int)fbytes, 0x00020000);
-  };
-  const __amdgpu_buffer_rsrc_t ry = rsrc(a.y);
-  auto voff = [&](int it) {
-    const int yy = y0 + (it >> 1), xx = x0 + row0 + 16 * (it & 1);
-    return (yy < H && xx < W) ? (unsigned)(((yy * W + xx) * 256 + q * 8) * 2) : 0x80000000u;
-  };
-  const bool up2 = a.r2h > 0;
-  const h16* pres2 = up2 ? nullptr : a.res2;  // a same-grid res2
-  const int nres = (a.res ? 1 : 0) + (pres2 ? 1 : 0);
-  const h16* r1p = a.res ? a.res : pres2;
-  const __amdgpu_buffer_rsrc_t rr1 = rsrc(r1p ? r1p : a.y);
-  const __amdgpu_buffer_rsrc_t rr2 = rsrc(pres2 ? pres2 : a.y);
-  // upsampled res2: the 4 source pixels of output pixel `it` (clamped into the map: rows past H / W
-  // are never stored) and its weights, as vda_upsample_bilinear forms them
-  const __amdgpu_buffer_rsrc_t rs2 = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)((up2 ? a.res2 : a.y) + (up2 ? (long)bt * a.r2h * a.r2w * 256 : fbase)), (short)0,
-      up2 ? (int)((long)a.r2h * a.r2w * 512) : (int)fbytes, 0x00020000);
-  const float usy = a.r2h > 0 && H > 1 ? (float)(a.r2h - 1) / (float)(H - 1) : 0.f;
-  const float usx = a.r2w > 0 && W > 1 ? (float)(a.r2w - 1) / (float)(W - 1) : 0.f;
-  auto up_load = [&](int it, h8* t4, float& wx, float& wy) {
-    const int yy = min(y0 + (it >> 1), H - 1), xx = min(x0 + row0 + 16 * (it & 1), W - 1);
-    const float fy = usy * (float)yy, fx = usx * (float)xx;
-    const int sy0 = (int)fy, sx0 = (int)fx;
-    const int sy1 = min(sy0 + 1, a.r2h - 1), sx1 = min(sx0 + 1, a.r2w - 1);
-    wy = fy - (float)sy0;
-    wx = fx - (float)sx0;
-    const unsigned r0 = (unsigned)(sy0 * a.r2w), r1 = (unsigned)(sy1 * a.r2w), c8 = (unsigned)q * 16u;
-    t4[0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx0) * 512u + c8, 0, 0));
-    t4[1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx1) * 512u + c8, 0, 0));
-    t4[2] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r1 + sx0) * 512u + c8, 0, 0));
-    t4[3] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r1 + sx1) * 512u + c8, 0, 0));
-  };
-  constexpr int UPD = 2;  // upsampled-res2 prefetch depth (pixels)
-  h8 u4[UPD][4];
-  float uwx[UPD], uwy[UPD];
-  if (up2) {
-#pragma unroll
-    for (int it = 0; it < UPD; ++it) up_load(it, u4[it], uwx[it], uwy[it]);
-  }
-  constexpr int PD = 4;
-  h8 q1[PD], q2[PD];
-  if (nres >= 1) {
-#pragma unroll
-    for (int it = 0; it < PD; ++it) q1[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr1, voff(it), 0, 0));
-  }
-  if (nres >= 2) {
-#pragma unroll
-    for (int it = 0; it < PD; ++it) q2[it] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rr2, voff(it), 0, 0));
-  }
-#endif
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const uint2 lo = *reinterpret_cast<const uint2*>(l0 + it * 16 * 256);

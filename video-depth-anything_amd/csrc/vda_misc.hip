@@ -29,15 +29,8 @@ extern "C" const char* vda_version(void) { return "libvda 0.2 (gfx950, fp16 MFMA
 extern "C" int64_t vda_epilogue_size(void) { return (int64_t)sizeof(vda_epilogue); }
 extern "C" const char* vda_last_error(void) { return g_err; }
 
-// upsample tuning (A/B builds): outputs per thread, non-temporal output stores.  Measured
-// (tools/bench_upsample.py, 2 rounds): nt stores -4 % at 148->296 / 296->518, -24 % at 74->148;
-// 4 outputs per thread slower than 2
-#ifndef VDA_UP_UNROLL
-#define VDA_UP_UNROLL 2
-#endif
-#ifndef VDA_UP_NT
-#define VDA_UP_NT 1
-#endif
+// upsample: 2 outputs per thread, non-temporal output stores.  Measured (tools/archive/bench_upsample.py,
+// 2 rounds): nt stores -4 % at 148->296 / 296->518, -24 % at 74->148; 4 outputs per thread slower than 2
 
 namespace {
 
@@ -89,11 +82,7 @@ __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x
         const unsigned i = i0 + u * 256u;
         if (i < row_items) {
           const h8 o = bilerp8(a[u], b[u], c[u], d[u], wx[u], wy);
-#if VDA_UP_NT
           __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(out + (long)i * 8));
-#else
-          stg16(out + (long)i * 8, __builtin_bit_cast(uint4, o));
-#endif
         }
       }
     }
@@ -138,7 +127,7 @@ extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t
                                      int32_t Ho, int32_t Wo, void* stream) {
   VDA_CHECK_ARG(x && y, "null pointer");
   VDA_CHECK_ARG(BT > 0 && H > 0 && W > 0 && Ho > 0 && Wo > 0 && C > 0 && C % 8 == 0, "bad resize geometry");
-  constexpr int UP = VDA_UP_UNROLL;
+  constexpr int UP = 2;
   const long row_items = (long)Wo * (C / 8);
   VDA_CHECK_ARG(row_items < (1L << 30) && (long)W * C < (1L << 31), "resize row too wide");
   const int gx = (int)((row_items + 256 * UP - 1) / (256 * UP));

@@ -38,11 +38,7 @@ constexpr int ST_PPW = (ST_PP + 7) / 8;                     // per wave, fixed (
 constexpr int ST_PBUF = ST_PPW * 8 * 512;                   // halfs per patch ring slot (56 KiB)
 constexpr int ST_N = 256;                                   // output channels
 constexpr int ST_WBUF = ST_N * ST_CPX * 8;                  // halfs per weight step (16 KiB)
-#ifdef ST_W2
-constexpr int ST_WR = 2;                                    // weight ring slots (A/B: the round-1 ring)
-#else
 constexpr int ST_WR = 3;                                    // weight ring: step t+2's weights in flight
-#endif
 
 struct StripParams {
   const h16* x;
@@ -232,13 +228,12 @@ __global__ __launch_bounds__(512) void strip_conv_kernel(StripParams p) {
       }
       // compiler-visible vmcnt(0) once per work item: without it the loads / stores above stay
       // "pending" across the loop back-edge and hipcc put an s_waitcnt vmcnt(0) before the first VGPR
-      // write of every step (draining the weight ring)
+      // write of every step (draining the weight ring).  It also drains the ring prefetch in flight
+      // here (step t+2's weights, and at tap 8 any issued patch pieces): a per-item cost, measured
+      // cheaper than the per-step drains it replaces (profiles/r04_ab_strip_wring3.log)
       __builtin_amdgcn_s_waitcnt(0x0F70);
     }
-    if constexpr (ST_WR == 2) {
-      if (issue_p) st_wait<ST_PPW>();
-      else st_wait<0>();
-    } else {
+    {
       // step gs + 1's weights must have landed; newer than them: this step's weights (2 pieces) and
       // the next unit's patch pieces when issued this step (after the weights) or the previous step
       // (tap 1: before this step's weights; they then land by the end of tap 1, 8 steps early)

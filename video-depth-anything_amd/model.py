@@ -535,8 +535,8 @@ class VideoDepthAnything(nn.Module):
         nparts = (C + 255) // 256
         epistats = P.lnfold and nparts <= 4 and bool(self.epilogue_stats)
         if epistats:
-            # one spare row: the LN-folded GEMMs stage the partials in 16-byte pieces (vda.h ln_parts)
-            st_a = torch.empty(tok.shape[0] + 1, nparts, 2, device=tok.device, dtype=torch.float32)
+            # [M, P, 2] exactly: the LN-folded GEMMs never read past it (vda.h ln_parts)
+            st_a = torch.empty(tok.shape[0], nparts, 2, device=tok.device, dtype=torch.float32)
             st_b = torch.empty_like(st_a)
         stats, parts = None, 0
         for i, q in enumerate(P.blocks):
