@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="clips in flight per GPU: step i runs on HIP stream i %% streams (the fc1 roofline "
                          "probe then runs in a single-stream pass after the timed region)")
+    ap.add_argument("--tiles", choices=["model", "static", "dynamic"], default="model",
+                    help="A/B: the encoder GEMMs' tile schedule (model = the model's default)")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip the per-step depth gather to rank 0")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo for rehearsal)")
     ap.add_argument("--dry-run", action="store_true",
@@ -164,6 +166,8 @@ def main():
         # (the recipe is deterministic, so every rank could build it; the broadcast is the deployment
         # path for a checkpoint that only rank 0 reads)
         model = vda_amd.build_model(enc, device=dev)
+        if args.tiles != "model":
+            model.dynamic_tiles = args.tiles == "dynamic"
     if dist:
         for t in model.state_dict().values():
             if args.backend == "nccl":

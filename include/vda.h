@@ -90,6 +90,13 @@ typedef struct vda_epilogue {
    * bit-identical to vda_upsample_bilinear + the add; ldres2 is then the source row stride (= N).
    * Served where vda_conv2d_res2_upsample_ok says so (the halo-tiled 256-channel conv); 0 = same grid. */
   int32_t res2_h, res2_w;
+  /* Optional tile scheduler of the persistent 256x256 GEMM: 9 int32, zero before the first launch and
+   * left zero by every launch (the last block to finish clears them).  Blocks then take their tiles
+   * beyond the first round by atomic ticket (per XCD) instead of a fixed stride, so blocks that start
+   * late (the GPU shared with another stream's kernels) run fewer tiles.  A counter set must not be used
+   * by two launches that can run at the same time (one per stream).  NULL: static schedule.  Ignored by
+   * the other kernel routes. */
+  int32_t* sched;
 } vda_epilogue;
 
 /* Version / diagnostics. */

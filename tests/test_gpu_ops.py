@@ -849,3 +849,53 @@ def test_gemm_layernorm_fold_stress_statistics(kind, N2, act):
     err = rel(ya, ref)
     print(f"LN fold stress {kind} N={N2} act={act}: rel-L1 {err:.2e}, max rstd rel err {rstd_err:.2e}")
     assert err < 1e-3
+
+
+@pytest.mark.parametrize("M,N,K,kind", [(43840, 3072, 1024, "lnf"), (43840, 1024, 1024, "res"), (43840, 4096, 1024, "lnf_gelu"),
+                                        (43840, 1024, 4096, "res"), (8192, 1024, 512, "plain"), (20000, 768, 256, "res")])
+def test_gemm_dynamic_tile_schedule(M, N, K, kind):
+    """the persistent GEMM taking its tiles beyond the first round by per-XCD atomic
+    ticket (vda_epilogue.sched) computes every tile exactly as the fixed-stride schedule does
+    (torch.equal, statistics too), leaves the counters zero for the next launch, and two streams with
+    their own counter sets running the same GEMMs concurrently agree with it."""
+    g = torch.Generator().manual_seed(M + N + K)
+    x = (torch.randn(M, K, generator=g) * 0.5).half().to(DEV)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).half().to(DEV)
+    b = f32(0.1 * torch.randn(N, generator=g))
+    kw = dict(bias=b)
+    if kind.startswith("lnf"):
+        xf = x.float().view(M, K // 256, 256)
+        kw.update(ln_stats=torch.stack([xf.sum(2), (xf * xf).sum(2)], 2).contiguous(), ln_parts=K // 256, ln_eps=1e-6,
+                  ln_colsum=w.float().sum(1).contiguous(), act=ACT_GELU if kind.endswith("gelu") else 0)
+    res = (torch.randn(M, N, generator=g)).half().to(DEV) if kind == "res" else None
+    P = (N + 255) // 256
+
+    def run(sched, stream=None):
+        out = res.clone() if res is not None else torch.empty(M, N, dtype=torch.float16, device=DEV)
+        so = torch.full((M, P, 2), float("nan"), device=DEV) if res is not None else None
+        ops.gemm(x, w, res=out if res is not None else None, out=out, stats_out=so, sched=sched, **kw)
+        return out, so
+
+    y0, s0 = run(None)
+    sch = torch.zeros(16, dtype=torch.int32, device=DEV)
+    for _ in range(3):
+        y1, s1 = run(sch)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y0)
+        if s0 is not None:
+            assert torch.equal(s1, s0)
+        assert int(sch.abs().sum()) == 0, "the last block must leave the counters zero"
+    # two streams, own counters, interleaved launches
+    st = [torch.cuda.Stream(), torch.cuda.Stream()]
+    cs = [torch.zeros(16, dtype=torch.int32, device=DEV) for _ in st]
+    torch.cuda.synchronize()
+    outs = []
+    for r in range(4):
+        with torch.cuda.stream(st[r % 2]):
+            outs.append(run(cs[r % 2])[0])
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, y0)
+    assert all(int(c.abs().sum()) == 0 for c in cs)
+    # the model's per-stream counter sets
+    assert ops.sched_counters().dtype == torch.int32 and ops.sched_counters() is ops.sched_counters()

@@ -53,7 +53,7 @@ class Epilogue(ctypes.Structure):
         ("ldres2", c_int64), ("act", c_int32), ("store", c_int32), ("ps_k", c_int32),
         ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
         ("ln_stats", c_void_p), ("ln_colsum", c_void_p), ("ln_parts", c_int32), ("ln_eps", c_float),
-        ("stats_out", c_void_p), ("res2_h", c_int32), ("res2_w", c_int32),
+        ("stats_out", c_void_p), ("res2_h", c_int32), ("res2_w", c_int32), ("sched", c_void_p),
     ]
 
 

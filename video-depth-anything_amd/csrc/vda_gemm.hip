@@ -426,6 +426,28 @@ __device__ __forceinline__ void lds_st_f2(float* ptr, float2 v) {
   asm volatile("ds_write_b64 %0, %1" ::"v"((unsigned)(uintptr_t)(VDA_LDS float*)ptr), "v"(v) : "memory");
 }
 
+// Dynamic tile schedule (vda_epilogue.sched): one agent-scope ticket draw per tile, through asm so that
+// the compiler's vmcnt bookkeeping never waits for it (the counted DMA waits that follow retire it: it is
+// older than the pieces they leave in flight), and the slot it is published to in LDS.
+__device__ __forceinline__ unsigned ticket_draw(unsigned* ctr) {
+  unsigned v;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=v"(v) : "v"(ctr), "v"(1u) : "memory");
+  return v;
+}
+// publishes tile base + 8 v; v (the draw's asm output) is read only inside this asm, after the counted
+// wait that retired the draw, so no compiler-scheduled use of it can run before the value has landed
+__device__ __forceinline__ void ticket_publish(int* ptr, unsigned v, int base) {
+  unsigned t;
+  asm volatile("v_lshl_add_u32 %0, %1, 3, %2\n\tds_write_b32 %3, %0" : "=&v"(t)
+               : "v"(v), "s"(base), "v"((unsigned)(uintptr_t)(VDA_LDS int*)ptr) : "memory");
+}
+__device__ __forceinline__ int lds_ld_i1(const int* ptr) {
+  int v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v)
+               : "v"((unsigned)(uintptr_t)(VDA_LDS const int*)ptr) : "memory");
+  return v;
+}
+
 __device__ __forceinline__ void glds16(const void* src, h16* lds_base) {
   __builtin_amdgcn_global_load_lds(src, (VDA_LDS void*)lds_base, 16, 0, 0);
 }
@@ -701,8 +723,13 @@ constexpr int phased_nit() {
 // the epilogue, which keeps the uniform state of the persistent loop in SGPRs (no spill reloads,
 // whose vmcnt(0) would drain the chained stores at every tile start).
 template <int XR, int WR, bool CONV, int ACT, bool ROWB, bool LNF, int EK>  // X / W operand regions of 128 rows (BM = 128 XR, BN = 128 WR)
-__device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem,
-                                             bool pre, int vb_next, int wave_in) {
+__device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int tiles_m, int tiles_n, h16* smem,
+                                            bool pre, int vb_next, int wave_in, unsigned* tctr = nullptr,
+                                            int tbase = 0, int* tslot = nullptr) {
+  // vb_next: the static successor (vb + grid, or -1).  tctr: dynamic schedule (this block's XCD ticket
+  // counter): wave 0 draws ticket v in K step 0's P3 and publishes tile tbase + 8 v in *tslot after that
+  // step's P4 wait; every wave reads it after the main loop.  Returns the tile this block runs next (or -1);
+  // only the fixed-kind epilogues (EK != 0) chain its prologue.
   // ROWB: per-row bias support (a separate instantiation: its row-index division would otherwise
   // raise the register pressure of every phased GEMM past the spill point)
   // LNF: LayerNorm folded into the GEMM (vda_epilogue.ln_stats / ln_colsum): X is the raw residual
@@ -1056,6 +1083,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     __builtin_amdgcn_s_barrier();
   };
 
+  unsigned tk = 0;  // dynamic schedule: the ticket in flight (wave 0, lane 0)
   // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
   // and retired by the P4 wait one phase before its first read:
   //   P1: Xq1(t+1) -> other buffer   P2: Wq0(t+1) -> other   P3: Xq0(t+2) -> this   P4: Wq1(t+2) -> this
@@ -1072,8 +1100,12 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     load_w(base, 1);
     if (more1) stage_w(kt + 1, nb, 0);
     mma(0, 1);
-    // P3
+    // P3 (dynamic schedule: wave 0 draws the successor's ticket here, ahead of the quarters the P4 wait
+    // leaves in flight, so that wait retires it)
     load_x(base, 1);
+    if (tctr != nullptr && wave == 0 && kt == 0) {
+      if (lane == 0) tk = ticket_draw(tctr);
+    }
     if (more2) stage_x(kt + 2, cb, 0);
     mma(1, 1);
     // P4: retire everything but this tile's two P3/P4 quarters
@@ -1084,10 +1116,20 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
     } else {
       wait_vmcnt<0>();
     }
+    if (tctr != nullptr && wave == 0 && kt == 0) {  // the draw has landed: publish the successor
+      if (lane == 0) ticket_publish(tslot, tk, tbase);
+    }
     mma(1, 0);
   }
   if (!lagging) __builtin_amdgcn_s_barrier();  // balance the stagger
   TS(3);
+  // the successor: published by wave 0 before step 0's last barrier (retired by the lgkmcnt waits after it)
+  int succ = vb_next;
+  if (tctr != nullptr) {
+    succ = __builtin_amdgcn_readfirstlane(lds_ld_i1(tslot));
+    if (succ >= tiles_m * tiles_n) succ = -1;
+  }
+  vb_next = EK != 0 ? succ : -1;  // the chained prologue
 
   const int mcol = lane & 15, nq = (lane >> 4) * 4;
   if constexpr ((EK == 1 || EK == 3) && XR == 2 && WR == 2) {
@@ -1203,7 +1245,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       __builtin_amdgcn_raw_buffer_store_b128(B, ry, rB, 0, VDA_EPI_STORE_AUX);
     }
     TS(5);
-    return;
+    return succ;
   }
   if constexpr (EK == 2 && XR == 2 && WR == 2) {
     // Register epilogue with one residual and the row statistics (proj, fc2: x += ...): the residual
@@ -1317,7 +1359,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rs, vo, 0, 0);
     }
     TS(5);
-    return;
+    return succ;
   }
   if (rows_store) {
     // LDS-staged epilogue: phase 1 writes t = gamma * act(acc + bias + rowbias) as fp16 into a
@@ -1625,14 +1667,14 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       phase2(std::integral_constant<int, 2>{});
     }
     TS(5);
-    return;
+    return succ;
   }
   if constexpr (PREF) {  // unused here: retire the prefetch loads inside the tile (no load pending across tiles)
 #pragma unroll
     for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(pbv[i]), "v"(pgv[i]));
   }
   if constexpr (EK != 0) {
-    return;  // row store only
+    return succ;  // row store only
   } else if constexpr (ACT == VDA_ACT_GEGLU) {
 #pragma unroll
     for (int i = 0; i < 4; i += 2) {
@@ -1657,6 +1699,7 @@ __device__ __forceinline__ void gemm256_tile(const GemmParams& p, int vb, int ti
       }
     }
   }
+  return succ;
 }
 
 // Persistent: one block per CU walks tiles vb, vb + gridDim.x, ... (virtual block ids keep the
@@ -1671,8 +1714,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
                                                       int desync) {
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
-  __shared__ __attribute__((aligned(1024))) h16 smem[2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 + 1024 : 0) +
-                                                     (EK == 2 ? 4096 : 0) + (EK == 3 ? 2048 : 0)];
+  // + 64 halves at the end (XR 2): the dynamic schedule's successor slot
+  constexpr int SMEM_HALVES = 2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 + 1024 : 0) + (EK == 2 ? 4096 : 0) +
+                              (EK == 3 ? 2048 : 0) + (XR == 2 ? 64 : 0);
+  __shared__ __attribute__((aligned(1024))) h16 smem[SMEM_HALVES];
   const int ntiles = tiles_m * tiles_n;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   if (desync > 1) {  // tuning experiment: every block starts ((b / 8) % desync) / desync of stagger_ticks late
@@ -1692,14 +1737,31 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     // the fixed-kind epilogues chain the next tile's prologue (gemm256_tile); the generic (EK 0) one
     // does not (chaining the staged row store measured 4 % slower on proj, 106.0 -> 110.3 us, round 3)
     const bool chain = EK != 0;
+    // dynamic schedule (vda_epilogue.sched; not with EK 3, whose row-bias slots follow the static tile
+    // order): a block's first tile is its id, the rest of its XCD's tiles (grid + xcd + 8 v) go by ticket
+    const bool dyn = XR == 2 && EK != 3 && p.epi.sched != nullptr && ntiles > (int)gridDim.x &&
+                     (gridDim.x & 7) == 0;
+    unsigned* tctr = dyn ? reinterpret_cast<unsigned*>(p.epi.sched) + (blockIdx.x & 7) : nullptr;
+    const int tbase = (int)gridDim.x + (int)(blockIdx.x & 7);
+    int* tslot = XR == 2 ? reinterpret_cast<int*>(smem + SMEM_HALVES - 64) : nullptr;
     bool pre = false;
-    for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
+    for (int vb = blockIdx.x; vb >= 0 && vb < ntiles;) {
       TS(0);
       const int nxt = vb + (int)gridDim.x;
-      gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, pre, chain && nxt < ntiles ? nxt : -1, wave);
+      vb = gemm256_tile<XR, WR, CONV, ACT, ROWB, LNF, EK>(p, vb, tiles_m, tiles_n, smem, pre, nxt < ntiles ? nxt : -1,
+                                                         wave, tctr, tbase, tslot);
       if (!chain) __syncthreads();
       pre = chain;
       TS(7);
+    }
+    if (dyn && wave == 0 && threadIdx.x == 0) {
+      // the block has drawn its last ticket (retired by its tile's waits): the last block to leave zeroes
+      // the counters for the next launch on this stream
+      unsigned* sc = reinterpret_cast<unsigned*>(p.epi.sched);
+      if (__hip_atomic_fetch_add(sc + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) __hip_atomic_store(sc + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 }

@@ -113,7 +113,7 @@ vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, in
 // ---- linear / 1x1 conv / ConvTranspose(k=s) ------------------------------------------------------
 Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
                  OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-                 OptT stats_out, Tensor out) {
+                 OptT stats_out, OptT sched, Tensor out) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "vda gemm: x must be a 2-D row-major (possibly row-strided) matrix");
   need_contig(w, dt, "w", x);
@@ -131,6 +131,11 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
   const at::OptionalDeviceGuard g(x.device());
   vda_epilogue e = make_epi(x, bias, rowbias, rdiv, rmod, gamma, res, res2, act, dt, ln_stats, ln_colsum, ln_parts,
                             ln_eps, stats_out);
+  if (sched) {  // the caller's per-stream tile-scheduler counters (vda.h vda_epilogue.sched)
+    need_contig(*sched, at::kInt, "sched", x);
+    TORCH_CHECK(sched->numel() >= 9, "vda gemm: sched must hold >= 9 int32 counters");
+    e.sched = (int32_t*)sched->data_ptr();
+  }
   const int rc = dt == at::kHalf
                      ? vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), (int32_t)M,
                                 (int32_t)N, (int32_t)K, &e, stream_of(x))
@@ -143,20 +148,20 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
 
 Tensor gemm(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
             OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-            OptT stats_out) {
+            OptT stats_out, OptT sched) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "vda gemm: x and w must be 2-D");
   const int64_t nout = act == VDA_ACT_GEGLU ? w.size(0) / 2 : w.size(0);
   Tensor out = at::empty({x.size(0), nout}, x.options().dtype(dt));
   return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps,
-                   stats_out, out);
+                   stats_out, sched, out);
 }
 
 Tensor& gemm_out(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
                  OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-                 OptT stats_out, Tensor& out) {
+                 OptT stats_out, OptT sched, Tensor& out) {
   gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps, stats_out,
-            out);
+            sched, out);
   return out;
 }
 
@@ -448,11 +453,12 @@ Tensor depth_resize(const Tensor& depth, int64_t ho, int64_t wo) {
 TORCH_LIBRARY(vda, m) {
   m.def("gemm(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
-        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None) -> Tensor");
+        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, "
+        "Tensor(c!)? sched=None) -> Tensor");
   m.def("gemm.out(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
-        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, *, "
-        "Tensor(a!) out) -> Tensor(a!)");
+        "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, "
+        "Tensor(c!)? sched=None, *, Tensor(a!) out) -> Tensor(a!)");
   m.def("row_stats(Tensor x, float eps) -> Tensor");
   m.def("conv_transpose_ks(Tensor x, Tensor w, Tensor bias, int BT, int h, int w_, int k) -> Tensor");
   m.def("conv2d(Tensor x, Tensor w, int ks=3, int stride=1, int pad=1, Tensor? bias=None, bool pre_relu=False, "

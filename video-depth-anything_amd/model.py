@@ -237,10 +237,13 @@ class VideoDepthAnything(nn.Module):
     of the packed-weight cache key): ``fold_layernorms`` folds the encoder's norm1 / norm2 into the
     qkv / fc1 GEMMs and the motion modules' attention-block LayerNorms into their q/k/v GEMMs (fp16
     mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
-    proj / fc2 epilogues instead of a separate pass.  No environment variable changes the schedule."""
+    proj / fc2 epilogues instead of a separate pass, ``dynamic_tiles`` lets the encoder's persistent GEMMs
+    take their tiles by atomic ticket (per-stream counters, ``ops.sched_counters``) instead of a fixed
+    stride.  No environment variable changes the schedule."""
 
     fold_layernorms: bool = True
     epilogue_stats: bool = True
+    dynamic_tiles: bool = False
 
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
@@ -539,29 +542,31 @@ class VideoDepthAnything(nn.Module):
             st_a = torch.empty(tok.shape[0], nparts, 2, device=tok.device, dtype=torch.float32)
             st_b = torch.empty_like(st_a)
         stats, parts = None, 0
+        sch = ops.sched_counters(tok.device) if self.dynamic_tiles and P.dt == torch.float16 else None
         for i, q in enumerate(P.blocks):
             if P.lnfold:  # norm1 folded into the qkv GEMM (statistics only)
                 if stats is None:
                     stats, parts = ops.row_stats(tok, 1e-6), 0
                 qkv = ops.gemm(tok, q.qkv_w, bias=q.qkv_b, ln_stats=stats, ln_parts=parts, ln_eps=1e-6,
-                               ln_colsum=q.qkv_c1)
+                               ln_colsum=q.qkv_c1, sched=sch)
             else:
                 qkv = ops.gemm(ops.layernorm(tok, q.n1w, q.n1b, 1e-6), q.qkv_w, bias=q.qkv_b)
             at = ops.spatial_attention(qkv, BT, ntok, P.heads, 64)
             del qkv
-            ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok, stats_out=st_a if epistats else None)
+            ops.gemm(at, q.proj_w, bias=q.proj_b, res=tok, out=tok, stats_out=st_a if epistats else None, sched=sch)
             if P.lnfold:  # norm2 folded into the fc1 GEMM
                 if epistats:
                     stats, parts = st_a, nparts
                 else:
                     stats, parts = ops.row_stats(tok, 1e-6), 0
                 f = ops.gemm(tok, q.fc1_w, bias=q.fc1_b, act=ACT_GELU, ln_stats=stats, ln_parts=parts, ln_eps=1e-6,
-                             ln_colsum=q.fc1_c1, tag="enc_fc1")
+                             ln_colsum=q.fc1_c1, sched=sch, tag="enc_fc1")
             else:
                 f = ops.gemm(ops.layernorm(tok, q.n2w, q.n2b, 1e-6), q.fc1_w, bias=q.fc1_b, act=ACT_GELU,
                              tag="enc_fc1")
             last = i + 1 == len(P.blocks)
-            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok, stats_out=st_b if epistats and not last else None)
+            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok, stats_out=st_b if epistats and not last else None,
+                     sched=sch)
             stats, parts = (st_b, nparts) if epistats else (None, 0)
             del f
             if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)

@@ -56,13 +56,15 @@ def _need(t: Tensor, dtype, name: str):
 
 def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
          res2=None, act=ACT_NONE, ln_stats=None, ln_colsum=None, ln_parts=0, ln_eps=1e-6, stats_out=None,
-         out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
+         sched=None, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
     """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view.
     fp16 x/w -> vda_gemm; fp32 x/w -> vda_gemm_f32 (fp32 mode).  torch.ops.vda.gemm[.out].
     ``ln_stats`` + ``ln_colsum`` fold a LayerNorm of x into the GEMM (vda.h): ln_stats is either
     ``row_stats(x)`` ([M, 2] (mean, rstd), ln_parts=0) or the [M, P, 2] partial sums another GEMM wrote
     through ``stats_out`` while producing x (ln_parts=P, ln_eps the LayerNorm eps).  ``stats_out``
-    ([M, ceil(N/256), 2] fp32) receives this GEMM's per-row partial (sum, sumsq) of its output."""
+    ([M, ceil(N/256), 2] fp32) receives this GEMM's per-row partial (sum, sumsq) of its output.
+    ``sched`` (int32 [>= 9], zeroed once; see ``sched_counters``) lets the persistent 256x256 GEMM take its
+    tiles by atomic ticket; one counter set per stream (vda.h vda_epilogue.sched)."""
     _need(x, x.dtype, "x")
     probe = _PROBE is not None and tag in _PROBE
     if probe:
@@ -71,14 +73,31 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
     v = _vda()
     if out is None:
         out = v.gemm(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum,
-                     int(ln_parts), float(ln_eps), stats_out)
+                     int(ln_parts), float(ln_eps), stats_out, sched)
     else:
         v.gemm.out(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum,
-                   int(ln_parts), float(ln_eps), stats_out, out=out)
+                   int(ln_parts), float(ln_eps), stats_out, sched, out=out)
     if probe:
         ev1.record()
         _PROBE[tag].append((ev0, ev1, 2.0 * x.shape[0] * w.shape[0] * x.shape[1]))
     return out
+
+
+_SCHED = {}
+
+
+def sched_counters(device=None) -> Tensor:
+    """The tile-scheduler counters (int32 [16], zero) of the current stream on `device`: one set per
+    stream, so that GEMMs on different streams never share one (vda_epilogue.sched).  The kernels leave
+    them zero after every launch."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    st = torch.cuda.current_stream(dev)
+    key = (dev.index, st.cuda_stream)
+    t = _SCHED.get(key)
+    if t is None:
+        t = torch.zeros(16, dtype=torch.int32, device=dev)
+        _SCHED[key] = t
+    return t
 
 
 def conv_transpose_ks(x: Tensor, w: Tensor, bias: Tensor, BT: int, h: int, w_: int, k: int) -> Tensor:
