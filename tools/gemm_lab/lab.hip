@@ -725,6 +725,558 @@ __global__ __launch_bounds__(256) void stage_probe_kernel(LabParams p, int tiles
   if (acc[0] == 0x12345678u && acc[1] == 7) sink[0] = 1.f;
 }
 
+
+// ---- w8: the product's 8-wave layout (2 m x 4 n waves, 128 x 64 wave tiles, 2 waves per SIMD) on the w4c
+// pipeline: NST-stage BK=32 ring, one barrier per step, DMA / fragment reads / MFMAs placed by hand ----
+template <int FL, int NST>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void w8_kernel(LabParams p, int tiles_m, int tiles_n) {
+  constexpr bool LB = NST * STAGE + 1024 <= 81920 && !(FL & 8);
+  __shared__ __attribute__((aligned(1024))) h16 smem[NST * STAGE + (LB ? 1024 : 0)];
+  constexpr int BOFS = NST * STAGE;
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = p.K / BK;
+  const i4v xrs = rsrc4(p.x, (long)p.M * p.K * 2), wrs = rsrc4(p.w, (long)p.N * p.K * 2);
+  const i4v brs = rsrc4(p.bias, (long)p.N * 4);
+  const int prow = lane >> 2;
+  const int pch = (lane & 3) ^ swz(prow);
+  const int frow = lane & 15, fch = lane >> 4;
+  const unsigned fofs = (unsigned)(frow * BK + ((fch ^ swz(frow)) << 3)) * 2u;
+  const unsigned xfo = fofs + (unsigned)(wm * 128 * BK * 2);
+  const unsigned wfo = fofs + (unsigned)((256 + wn * 64) * BK * 2);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(VDA_LDS h16*)smem);
+
+  f4 acc[4][8];
+  h8 fx[2][8], fw[2][4];
+  int vb = blockIdx.x;
+  unsigned xo[2], wo[2], bo = 0;
+  int cnt = 0;
+  auto offsets = [&](int vb_) {
+    int tm, tn;
+    tile_coords(vb_, ntiles, tiles_m, tiles_n, tm, tn);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wave * 2 + i) * 16 + prow;
+      const int m = tm * 256 + r, n = tn * 256 + r;
+      xo[i] = m < p.M ? (unsigned)(((long)m * p.K + pch * 8) * 2) : 0x80000000u;
+      wo[i] = n < p.N ? (unsigned)(((long)n * p.K + pch * 8) * 2) : 0x80000000u;
+    }
+    const int nb = tn * 256 + lane * 4;
+    bo = nb < p.N ? (unsigned)(nb * 4) : 0x80000000u;
+  };
+  auto piece = [&](int t, int q) {  // piece q (0..3) of step t: X pieces 0-1, W pieces 2-3
+    const unsigned sb = lds0 + (unsigned)((t % NST) * STAGE * 2);
+    if (q < 2) dma16(xrs, xo[q], t * BK * 2, sb + (unsigned)((wave * 2 + q) * 1024));
+    else dma16(wrs, wo[q - 2], t * BK * 2, sb + (unsigned)((256 * BK + (wave * 2 + q - 2) * 512) * 2));
+  };
+  auto prologue = [&](int slot) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) piece(s, q);
+    if (LB && wave == 0) dma16(brs, bo, 0, lds0 + (unsigned)((BOFS + slot * 512) * 2));
+  };
+  if (vb < ntiles) {
+    offsets(vb);
+    prologue(0);
+  }
+  for (; vb < ntiles; vb += gridDim.x, ++cnt) {
+    int tm, tn;
+    tile_coords(vb, ntiles, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    constexpr int YP = (NST - 1) * 4;
+    if (vb == (int)blockIdx.x) {
+      if (LB && wave == 0) wait_vm<YP + 1>(); else wait_vm<YP>();
+    } else {
+      if (LB && wave == 0) wait_vm<YP + 17>(); else wait_vm<YP + 16>();
+    }
+    __builtin_amdgcn_s_barrier();
+    {
+      const h16* sb = smem;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fx[0][j] = lds_frag(sb, xfo + j * 16 * BK * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fw[0][i] = lds_frag(sb, wfo + i * 16 * BK * 2);
+    }
+    const int vb_next = vb + (int)gridDim.x;
+
+    auto step = [&](int t, auto setc, auto waitc, auto dmac, auto readc, auto zc) {
+      constexpr int S = decltype(setc)::value;
+      constexpr int WAIT = decltype(waitc)::value;
+      constexpr int DMA = decltype(dmac)::value;
+      constexpr bool READ = decltype(readc)::value;
+      constexpr bool Z = decltype(zc)::value;
+      if constexpr (WAIT >= 0) wait_vm<WAIT>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      if constexpr (DMA == 2) {
+        if (vb_next < ntiles) {
+          offsets(vb_next);
+          prologue((cnt + 1) & 1);
+        }
+      }
+      const h16* sb = smem + ((t + 1) % NST) * STAGE;
+#pragma unroll
+      for (int mi = 0; mi < 32; ++mi) {
+        const int i = mi >> 3, j = mi & 7;
+        if constexpr (FL & 2) {
+          if (mi == 0) mfma_m(acc[i][j], fw[S][i], fx[S][j]);
+        } else if constexpr (Z) mfma_z(acc[i][j], fw[S][i], fx[S][j]);
+        else mfma_m(acc[i][j], fw[S][i], fx[S][j]);
+        if constexpr (READ && !(FL & 4)) {
+          if (mi % 2 == 0 && mi / 2 < 12) {
+            const int r = mi / 2;
+            if (r < 8) fx[S ^ 1][r] = lds_frag(sb, xfo + r * 16 * BK * 2);
+            else fw[S ^ 1][r - 8] = lds_frag(sb, wfo + (r - 8) * 16 * BK * 2);
+          }
+        }
+        if constexpr (DMA == 1 && !(FL & 1)) {
+          if (mi % 8 == 3) piece(t + NST, mi / 8);
+        }
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using WS = std::integral_constant<int, 4 * (NST - 2)>;
+    using RT = std::integral_constant<bool, true>;
+    using FT = std::false_type;
+    step(0, I0{}, WS{}, I1{}, RT{}, std::true_type{});
+    int t = 1;
+    if constexpr (NST % 2 == 0) {
+      step(1, I1{}, WS{}, I1{}, RT{}, FT{});
+      t = 2;
+      for (; t < nk - NST; t += 2) {
+        step(t, I0{}, WS{}, I1{}, RT{}, FT{});
+        step(t + 1, I1{}, WS{}, I1{}, RT{}, FT{});
+      }
+    } else {
+      for (; t < nk - NST; t += 2) {
+        step(t, I1{}, WS{}, I1{}, RT{}, FT{});
+        step(t + 1, I0{}, WS{}, I1{}, RT{}, FT{});
+      }
+    }
+    [&]<int... U>(std::integer_sequence<int, U...>) {
+      (([&] {
+         constexpr int u = U;
+         using SU = std::integral_constant<int, (NST + u) & 1>;
+         if constexpr (u == NST - 1) {
+           step(nk - 1, SU{}, std::integral_constant<int, -1>{}, I2{}, std::false_type{}, FT{});
+         } else {
+           step(nk - NST + u, SU{}, std::integral_constant<int, 4 * (NST - u - 2 > 0 ? NST - u - 2 : 0)>{}, I0{}, RT{}, FT{});
+         }
+       }()), ...);
+    }(std::make_integer_sequence<int, NST>{});
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    const int mcol = lane & 15, g = lane >> 4;
+    const bool lo8 = (mcol & 8) == 0;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.y, (short)0, (int)((long)p.M * p.N * 2 < 0x7fffffffL ? (long)p.M * p.N * 2 : 0x7fffffffL), 0x00020000);
+    f4 bv[4];
+    {
+      const float* bl = reinterpret_cast<const float*>(smem + BOFS + (cnt & 1) * 512);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = LB ? *reinterpret_cast<const f4*>(bl + wn * 64 + i * 16 + g * 4) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      u32x4 o[2];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int ia = 2 * pp;
+        float a[4], c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = acc[ia][j][r] + bv[ia][r];
+          c[r] = acc[ia + 1][j][r] + bv[ia + 1][r];
+          perm16_swap(a[r], c[r]);
+        }
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
+        const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
+        o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                      __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+      }
+      u32x4 A, B;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned snd = lo8 ? o[1][k] : o[0][k];
+        const unsigned got = (unsigned)__builtin_amdgcn_mov_dpp((int)snd, 0x128, 0xF, 0xF, true);
+        A[k] = lo8 ? o[0][k] : got;
+        B[k] = lo8 ? got : o[1][k];
+      }
+      const int col = n0 + wn * 64 + 32 * (lo8 ? 0 : 1) + 16 * (g & 1) + 8 * (g >> 1);
+      const int rowA = m0 + wm * 128 + j * 16 + (mcol & 7);
+      const bool okc = col < p.N;
+      const unsigned oA = okc && rowA < p.M ? (unsigned)(((long)rowA * p.N + col) * 2) : 0x80000000u;
+      const unsigned oB = okc && rowA + 8 < p.M ? (unsigned)(((long)(rowA + 8) * p.N + col) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(A, ry, oA, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(B, ry, oB, 0, 2);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+// ---- w8b: w8 with the MFMAs in X-block-major order, ONE X fragment set (each X fragment of step t+1 read
+// right after the last MFMA of step t that uses its register) and two W sets: 64 fragment VGPRs instead of 96
+// ---- (w8: the product's 8-wave layout (2 m x 4 n waves, 128 x 64 wave tiles, 2 waves per SIMD) on the w4c
+// pipeline: NST-stage BK=32 ring, one barrier per step, DMA / fragment reads / MFMAs placed by hand ----
+template <int FL, int NST>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void w8b_kernel(LabParams p, int tiles_m, int tiles_n) {
+  constexpr bool LB = NST * STAGE + 1024 <= 81920 && !(FL & 8);
+  __shared__ __attribute__((aligned(1024))) h16 smem[NST * STAGE + (LB ? 1024 : 0)];
+  constexpr int BOFS = NST * STAGE;
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = p.K / BK;
+  const i4v xrs = rsrc4(p.x, (long)p.M * p.K * 2), wrs = rsrc4(p.w, (long)p.N * p.K * 2);
+  const i4v brs = rsrc4(p.bias, (long)p.N * 4);
+  const int prow = lane >> 2;
+  const int pch = (lane & 3) ^ swz(prow);
+  const int frow = lane & 15, fch = lane >> 4;
+  const unsigned fofs = (unsigned)(frow * BK + ((fch ^ swz(frow)) << 3)) * 2u;
+  const unsigned xfo = fofs + (unsigned)(wm * 128 * BK * 2);
+  const unsigned wfo = fofs + (unsigned)((256 + wn * 64) * BK * 2);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(VDA_LDS h16*)smem);
+
+  f4 acc[4][8];
+  h8 fx[8], fw[2][4];
+  int vb = blockIdx.x;
+  unsigned xo[2], wo[2], bo = 0;
+  int cnt = 0;
+  auto offsets = [&](int vb_) {
+    int tm, tn;
+    tile_coords(vb_, ntiles, tiles_m, tiles_n, tm, tn);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (wave * 2 + i) * 16 + prow;
+      const int m = tm * 256 + r, n = tn * 256 + r;
+      xo[i] = m < p.M ? (unsigned)(((long)m * p.K + pch * 8) * 2) : 0x80000000u;
+      wo[i] = n < p.N ? (unsigned)(((long)n * p.K + pch * 8) * 2) : 0x80000000u;
+    }
+    const int nb = tn * 256 + lane * 4;
+    bo = nb < p.N ? (unsigned)(nb * 4) : 0x80000000u;
+  };
+  auto piece = [&](int t, int q) {  // piece q (0..3) of step t: X pieces 0-1, W pieces 2-3
+    const unsigned sb = lds0 + (unsigned)((t % NST) * STAGE * 2);
+    if (q < 2) dma16(xrs, xo[q], t * BK * 2, sb + (unsigned)((wave * 2 + q) * 1024));
+    else dma16(wrs, wo[q - 2], t * BK * 2, sb + (unsigned)((256 * BK + (wave * 2 + q - 2) * 512) * 2));
+  };
+  auto prologue = [&](int slot) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) piece(s, q);
+    if (LB && wave == 0) dma16(brs, bo, 0, lds0 + (unsigned)((BOFS + slot * 512) * 2));
+  };
+  if (vb < ntiles) {
+    offsets(vb);
+    prologue(0);
+  }
+  for (; vb < ntiles; vb += gridDim.x, ++cnt) {
+    int tm, tn;
+    tile_coords(vb, ntiles, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    constexpr int YP = (NST - 1) * 4;
+    if (vb == (int)blockIdx.x) {
+      if (LB && wave == 0) wait_vm<YP + 1>(); else wait_vm<YP>();
+    } else {
+      if (LB && wave == 0) wait_vm<YP + 17>(); else wait_vm<YP + 16>();
+    }
+    __builtin_amdgcn_s_barrier();
+    {
+      const h16* sb = smem;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fx[j] = lds_frag(sb, xfo + j * 16 * BK * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fw[0][i] = lds_frag(sb, wfo + i * 16 * BK * 2);
+    }
+    const int vb_next = vb + (int)gridDim.x;
+
+    auto step = [&](int t, auto setc, auto waitc, auto dmac, auto readc, auto zc) {
+      constexpr int S = decltype(setc)::value;
+      constexpr int WAIT = decltype(waitc)::value;
+      constexpr int DMA = decltype(dmac)::value;
+      constexpr bool READ = decltype(readc)::value;
+      constexpr bool Z = decltype(zc)::value;
+      if constexpr (WAIT >= 0) wait_vm<WAIT>();
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+      if constexpr (DMA == 2) {
+        if (vb_next < ntiles) {
+          offsets(vb_next);
+          prologue((cnt + 1) & 1);
+        }
+      }
+      const h16* sb = smem + ((t + 1) % NST) * STAGE;
+#pragma unroll
+      for (int mi = 0; mi < 32; ++mi) {
+        const int j = mi >> 2, i = mi & 3;  // X-block-major: fx[j] is dead after MFMA (j, 3)
+        if constexpr (FL & 2) {
+          if (mi == 0) mfma_m(acc[i][j], fw[S][i], fx[j]);
+        } else if constexpr (Z) mfma_z(acc[i][j], fw[S][i], fx[j]);
+        else mfma_m(acc[i][j], fw[S][i], fx[j]);
+        if constexpr (READ && !(FL & 4)) {
+          if (i == 3) fx[j] = lds_frag(sb, xfo + j * 16 * BK * 2);           // step t+1's X block j
+          if (i == 1 && j < 4) fw[S ^ 1][j] = lds_frag(sb, wfo + j * 16 * BK * 2);  // step t+1's W block j
+        }
+        if constexpr (DMA == 1 && !(FL & 1)) {
+          if (mi % 8 == 5) piece(t + NST, mi / 8);
+        }
+      }
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using WS = std::integral_constant<int, 4 * (NST - 2)>;
+    using RT = std::integral_constant<bool, true>;
+    using FT = std::false_type;
+    step(0, I0{}, WS{}, I1{}, RT{}, std::true_type{});
+    int t = 1;
+    if constexpr (NST % 2 == 0) {
+      step(1, I1{}, WS{}, I1{}, RT{}, FT{});
+      t = 2;
+      for (; t < nk - NST; t += 2) {
+        step(t, I0{}, WS{}, I1{}, RT{}, FT{});
+        step(t + 1, I1{}, WS{}, I1{}, RT{}, FT{});
+      }
+    } else {
+      for (; t < nk - NST; t += 2) {
+        step(t, I1{}, WS{}, I1{}, RT{}, FT{});
+        step(t + 1, I0{}, WS{}, I1{}, RT{}, FT{});
+      }
+    }
+    [&]<int... U>(std::integer_sequence<int, U...>) {
+      (([&] {
+         constexpr int u = U;
+         using SU = std::integral_constant<int, (NST + u) & 1>;
+         if constexpr (u == NST - 1) {
+           step(nk - 1, SU{}, std::integral_constant<int, -1>{}, I2{}, std::false_type{}, FT{});
+         } else {
+           step(nk - NST + u, SU{}, std::integral_constant<int, 4 * (NST - u - 2 > 0 ? NST - u - 2 : 0)>{}, I0{}, RT{}, FT{});
+         }
+       }()), ...);
+    }(std::make_integer_sequence<int, NST>{});
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    const int mcol = lane & 15, g = lane >> 4;
+    const bool lo8 = (mcol & 8) == 0;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.y, (short)0, (int)((long)p.M * p.N * 2 < 0x7fffffffL ? (long)p.M * p.N * 2 : 0x7fffffffL), 0x00020000);
+    f4 bv[4];
+    {
+      const float* bl = reinterpret_cast<const float*>(smem + BOFS + (cnt & 1) * 512);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = LB ? *reinterpret_cast<const f4*>(bl + wn * 64 + i * 16 + g * 4) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      u32x4 o[2];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int ia = 2 * pp;
+        float a[4], c[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = acc[ia][j][r] + bv[ia][r];
+          c[r] = acc[ia + 1][j][r] + bv[ia + 1][r];
+          perm16_swap(a[r], c[r]);
+        }
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
+        const h2 h2_ = __builtin_convertvector(f2v{c[0], c[1]}, h2), h3 = __builtin_convertvector(f2v{c[2], c[3]}, h2);
+        o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                      __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+      }
+      u32x4 A, B;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned snd = lo8 ? o[1][k] : o[0][k];
+        const unsigned got = (unsigned)__builtin_amdgcn_mov_dpp((int)snd, 0x128, 0xF, 0xF, true);
+        A[k] = lo8 ? o[0][k] : got;
+        B[k] = lo8 ? got : o[1][k];
+      }
+      const int col = n0 + wn * 64 + 32 * (lo8 ? 0 : 1) + 16 * (g & 1) + 8 * (g >> 1);
+      const int rowA = m0 + wm * 128 + j * 16 + (mcol & 7);
+      const bool okc = col < p.N;
+      const unsigned oA = okc && rowA < p.M ? (unsigned)(((long)rowA * p.N + col) * 2) : 0x80000000u;
+      const unsigned oB = okc && rowA + 8 < p.M ? (unsigned)(((long)(rowA + 8) * p.N + col) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(A, ry, oA, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(B, ry, oB, 0, 2);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+
+// ---- w8r: register staging (buffer_load_dwordx4 -> VGPR -> ds_write_b128) of whole 128-B rows into a
+// 2-stage [256][64]-half ring (the product's swizzle), 8 waves (2 m x 4 n, 128 x 64 wave tiles), one
+// barrier per 64-deep step; MFMAs on AGPR accumulators (asm), X fragments rotated per block, two W sets.
+// (The staging probe measured whole-row VGPR loads at ~1.3x the LDS-DMA rate.)
+__device__ __forceinline__ unsigned swz64(int row, int chunk) {  // byte offset in a [rows][64 halves] image
+  return (unsigned)(row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4));
+}
+template <int FL>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void w8r_kernel(LabParams p, int tiles_m, int tiles_n) {
+  constexpr int RS = 512 * 64;  // halves per stage (X 256 rows + W 256 rows of 64)
+  __shared__ __attribute__((aligned(1024))) h16 smem[2 * RS];
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int tid = wave * 64 + lane;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = p.K / 64;
+  const __amdgpu_buffer_rsrc_t xrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)((long)p.M * p.K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, (int)((long)p.N * p.K * 2), 0x00020000);
+  // staging: thread -> chunk c = tid & 7 of rows r0 + 64 i (i = 0..3), for X and for W
+  const int c = tid & 7, r0 = tid >> 3;
+  const unsigned lw = swz64(r0, c);  // + i * 8192 (row + 64: the swizzle term repeats every 16 rows)
+  // fragments: row 16 blk + (lane & 15), 16-B chunk kh * 4 + (lane >> 4) of the 64-half row
+  const int frow = lane & 15, fch = lane >> 4;
+  unsigned fxo[2], fwo[2];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    fxo[kh] = swz64(wm * 128 + frow, kh * 4 + fch);
+    fwo[kh] = (unsigned)(256 * 128) + swz64(wn * 64 + frow, kh * 4 + fch);
+  }
+  f4 acc[4][8];
+  h8 fx[8], fw[2][4];
+  u32x4 R[4];
+  int vb = blockIdx.x;
+  unsigned xo = 0, wo = 0;
+  auto offsets = [&](int vb_) {
+    int tm, tn;
+    tile_coords(vb_, ntiles, tiles_m, tiles_n, tm, tn);
+    const int m = tm * 256 + r0, n = tn * 256 + r0;
+    xo = (unsigned)(((long)m * p.K + c * 8) * 2);
+    wo = (unsigned)(((long)n * p.K + c * 8) * 2);
+  };
+  // the staging in two halves (X rows, then W rows; 16 VGPRs): each half is loaded, then written to the
+  // next stage half a step later
+  auto gload = [&](int t, int half) {  // rows past M / N: past num_records -> zeros
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      R[i] = __builtin_amdgcn_raw_buffer_load_b128(half ? wrs : xrs, half ? wo : xo, i * 64 * p.K * 2 + t * 128, 0);
+  };
+  auto lstore = [&](int stage, int half) {
+    char* sb = reinterpret_cast<char*>(smem + stage * RS) + half * 256 * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x4*>(sb + lw + i * 8192) = R[i];
+  };
+  const char* s0 = reinterpret_cast<const char*>(smem);
+  auto xf = [&](int stage, int kh, int j) { return lds_frag(smem, stage * RS * 2 + fxo[kh] + j * 16 * 128); };
+  auto wf = [&](int stage, int kh, int i) { return lds_frag(smem, stage * RS * 2 + fwo[kh] + i * 16 * 128); };
+  (void)s0;
+  if (vb < ntiles) {
+    offsets(vb);
+    gload(0, 0);
+    lstore(0, 0);
+    gload(0, 1);
+  }
+  for (; vb < ntiles; vb += gridDim.x) {
+    int tm, tn;
+    tile_coords(vb, ntiles, tiles_m, tiles_n, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int vb_next = vb + (int)gridDim.x;
+    lstore(0, 1);  // step 0's second half (its first half was written by the previous tile's last step, or above)
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
+    for (int t = 0; t < nk; ++t) {
+      const int st = t & 1;
+      const bool more = t + 1 < nk, chain = !more && vb_next < ntiles;
+      if (more) gload(t + 1, 0);
+      else if (chain) { offsets(vb_next); gload(0, 0); }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fx[j] = xf(st, 0, j);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fw[0][i] = wf(st, 0, i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fw[1][i] = wf(st, 1, i);
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+#pragma unroll
+        for (int mi = 0; mi < 32; ++mi) {
+          const int j = mi >> 2, i = mi & 3;
+          if constexpr (FL & 2) {
+            if (mi == 0) mfma_m(acc[i][j], fw[kh][i], fx[j]);
+          } else if (t == 0 && kh == 0) mfma_z(acc[i][j], fw[kh][i], fx[j]);
+          else mfma_m(acc[i][j], fw[kh][i], fx[j]);
+          if (kh == 0 && i == 3) fx[j] = xf(st, 1, j);  // X block j of k-half 1
+        }
+        if (kh == 0) {  // mid-step: the X half of the next step's rows goes to the other stage, W is requested
+          if (more || chain) lstore(st ^ 1, 0);
+          if (more) gload(t + 1, 1);
+          else if (chain) gload(0, 1);
+        }
+      }
+      if (more) lstore(st ^ 1, 1);
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+
+    const int mcol = lane & 15, g = lane >> 4;
+    const bool lo8 = (mcol & 8) == 0;
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)p.y, (short)0, (int)((long)p.M * p.N * 2 < 0x7fffffffL ? (long)p.M * p.N * 2 : 0x7fffffffL), 0x00020000);
+    f4 bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + wn * 64 + i * 16 + g * 4;
+      bv[i] = n < p.N ? *reinterpret_cast<const f4*>(p.bias + n) : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      u32x4 o[2];
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int ia = 2 * pp;
+        float a[4], cc[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          a[r] = acc[ia][j][r] + bv[ia][r];
+          cc[r] = acc[ia + 1][j][r] + bv[ia + 1][r];
+          perm16_swap(a[r], cc[r]);
+        }
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const h2 h0 = __builtin_convertvector(f2v{a[0], a[1]}, h2), h1 = __builtin_convertvector(f2v{a[2], a[3]}, h2);
+        const h2 h2_ = __builtin_convertvector(f2v{cc[0], cc[1]}, h2), h3 = __builtin_convertvector(f2v{cc[2], cc[3]}, h2);
+        o[pp] = u32x4{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1),
+                      __builtin_bit_cast(unsigned, h2_), __builtin_bit_cast(unsigned, h3)};
+      }
+      u32x4 A, B;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned snd = lo8 ? o[1][k] : o[0][k];
+        const unsigned got = (unsigned)__builtin_amdgcn_mov_dpp((int)snd, 0x128, 0xF, 0xF, true);
+        A[k] = lo8 ? o[0][k] : got;
+        B[k] = lo8 ? got : o[1][k];
+      }
+      const int col = n0 + wn * 64 + 32 * (lo8 ? 0 : 1) + 16 * (g & 1) + 8 * (g >> 1);
+      const int rowA = m0 + wm * 128 + j * 16 + (mcol & 7);
+      const bool okc = col < p.N;
+      const unsigned oA = okc && rowA < p.M ? (unsigned)(((long)rowA * p.N + col) * 2) : 0x80000000u;
+      const unsigned oB = okc && rowA + 8 < p.M ? (unsigned)(((long)(rowA + 8) * p.N + col) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(A, ry, oA, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b128(B, ry, oB, 0, 2);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
 }  // namespace
 
 extern "C" int lab_gemm(int variant, const void* x, const void* w, void* y, const float* bias, int M, int N, int K,
@@ -754,6 +1306,15 @@ extern "C" int lab_gemm(int variant, const void* x, const void* w, void* y, cons
     case 31: hipLaunchKernelGGL((stage_probe_kernel<128, 0>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     case 32: hipLaunchKernelGGL((stage_probe_kernel<64, 1>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     case 33: hipLaunchKernelGGL((stage_probe_kernel<128, 1>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 40: hipLaunchKernelGGL((w8_kernel<0, 4>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 41: hipLaunchKernelGGL((w8_kernel<8, 5>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 42: hipLaunchKernelGGL((w8_kernel<6, 4>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 43: hipLaunchKernelGGL((w8_kernel<1, 4>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 44: hipLaunchKernelGGL((w8_kernel<5, 4>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 50: hipLaunchKernelGGL((w8b_kernel<0, 4>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 51: hipLaunchKernelGGL((w8b_kernel<8, 5>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 60: hipLaunchKernelGGL((w8r_kernel<0>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
+    case 62: hipLaunchKernelGGL((w8r_kernel<2>), dim3(g), dim3(512), 0, st, p, tiles_m, tiles_n); break;
     case 11: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 1>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;
     case 12: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 2>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;
     case 14: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 4>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;

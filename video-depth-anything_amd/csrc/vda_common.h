@@ -53,6 +53,13 @@ __device__ __forceinline__ float erf_fast(float x) {
 // Bilinear blend of 8 fp16 channels in fp32, rounded to fp16: (1-wy)*((1-wx)*a + wx*b) + wy*((1-wx)*c + wx*d)
 // with every product / fma spelled out, so the resize kernel and the depth head's fused patch builder
 // produce bit-identical values (no compiler contraction choices in between).
+// Bilinear (align_corners=True) blend weight of output coordinate o at source scale sc, source index
+// i0 = (int)(sc * o): the exact product minus i0 in one fma.  Spelled out so that every resize site
+// (upsample kernel, the fused-resize convs, the res2 gather, the implicit-GEMM loader) forms the same
+// bits whatever the compiler's contraction choice in its code shape (a restructured loop could keep the
+// rounded product instead and move w by an ulp: DESIGN.md §3, round-4 levers).
+__device__ __forceinline__ float ac_weight(float sc, float o, int i0) { return __builtin_fmaf(sc, o, -(float)i0); }
+
 __device__ __forceinline__ h8 bilerp8(h8 a, h8 b, h8 c, h8 d, float wx, float wy) {
   const float ux = 1.f - wx, uy = 1.f - wy;
   h8 o;

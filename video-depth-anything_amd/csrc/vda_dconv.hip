@@ -191,10 +191,11 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
         int sy0, sy1, sx0, sx1;
         float wy, wx;
         {
-          const float fy = usy * (float)min(max(py, 0), H - 1);
-          sy0 = (int)fy; sy1 = min(sy0 + 1, Hs - 1); wy = fy - (float)sy0;
-          const float fx = usx * (float)min(max(px, 0), W - 1);
-          sx0 = (int)fx; sx1 = min(sx0 + 1, Ws - 1); wx = fx - (float)sx0;
+          const float oy = (float)min(max(py, 0), H - 1), ox = (float)min(max(px, 0), W - 1);
+          const float fy = usy * oy;
+          sy0 = (int)fy; sy1 = min(sy0 + 1, Hs - 1); wy = ac_weight(usy, oy, sy0);
+          const float fx = usx * ox;
+          sx0 = (int)fx; sx1 = min(sx0 + 1, Ws - 1); wx = ac_weight(usx, ox, sx0);
         }
         const int r0 = (sy0 - sy_lo) * SC, r1 = (sy1 - sy_lo) * SC, c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
         const uint4 a = *reinterpret_cast<const uint4*>(ssm + ((r0 + c0) * 4 + cd) * 8);

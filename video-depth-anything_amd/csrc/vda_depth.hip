@@ -59,7 +59,7 @@ __device__ __forceinline__ void dh_ac_coord(int o, int in, float sc, int& i0, in
   const float f = sc * (float)o;
   i0 = (int)f;
   i1 = min(i0 + 1, in - 1);
-  w = f - (float)i0;
+  w = ac_weight(sc, (float)o, i0);
 }
 
 // DEPTH: the depth tail (64 weight rows = 32 hi + 32 lo, wave n-blocks {ng, ng+2}, ReLU/1x1/ReLU epilogue

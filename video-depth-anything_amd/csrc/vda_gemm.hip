@@ -133,7 +133,7 @@ struct ConvLoader {
       float fy = sy * iy, fx = sx * ix;
       int y0 = (int)fy, x0 = (int)fx;
       int y1 = min(y0 + 1, p.H - 1), x1 = min(x0 + 1, p.W - 1);
-      float wy = fy - y0, wx = fx - x0;
+      float wy = ac_weight(sy, (float)iy, y0), wx = ac_weight(sx, (float)ix, x0);
       const h16* base = p.x + (long)bt[i] * p.H * p.W * p.Cin + ci;
       h8 a = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * p.W + x0) * p.Cin));
       h8 b = __builtin_bit_cast(h8, ldg16(base + ((long)y0 * p.W + x1) * p.Cin));

@@ -334,8 +334,8 @@ __global__ __launch_bounds__(512) void hconv256_kernel(HconvArgs a) {
     const float fy = usy * (float)yy, fx = usx * (float)xx;
     const int sy0 = (int)fy, sx0 = (int)fx;
     const int sy1 = min(sy0 + 1, a.r2h - 1), sx1 = min(sx0 + 1, a.r2w - 1);
-    wy = fy - (float)sy0;
-    wx = fx - (float)sx0;
+    wy = ac_weight(usy, (float)yy, sy0);
+    wx = ac_weight(usx, (float)xx, sx0);
     const unsigned r0 = (unsigned)(sy0 * a.r2w), r1 = (unsigned)(sy1 * a.r2w), c8 = (unsigned)q * 16u;
     t4[0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx0) * 512u + c8, 0, 0));
     t4[1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs2, (r0 + sx1) * 512u + c8, 0, 0));

@@ -40,7 +40,7 @@ __device__ __forceinline__ void ac_coord(int o, int in, int out, int& i0, int& i
   const float f = sc * (float)o;
   i0 = (int)f;
   i1 = min(i0 + 1, in - 1);
-  w = f - (float)i0;
+  w = ac_weight(sc, (float)o, i0);
 }
 
 // One block row per output row (bt, oy): the two source rows and the y weight are fixed per block,
