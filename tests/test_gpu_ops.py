@@ -108,7 +108,10 @@ def test_gemm_strided_rows():
 
 @pytest.mark.parametrize("k,cin,cout,BT,hh,ww", [(4, 48, 48, 3, 5, 7), (2, 96, 96, 3, 5, 7), (4, 256, 256, 3, 5, 7),
                                                   # large M: the phased 256x256 kernel with the pixel-shuffle store
-                                                  (4, 256, 256, 4, 37, 37), (2, 512, 512, 4, 37, 37)])
+                                                  (4, 256, 256, 4, 37, 37), (2, 512, 512, 4, 37, 37),
+                                                  # the staged row epilogue's remapped whole-pixel stores (cout %
+                                                  # 256 == 0, w >= 16), ragged tiles and row wraps
+                                                  (4, 256, 256, 12, 19, 23), (2, 512, 512, 6, 17, 41)])
 def test_conv_transpose_pixel_shuffle(k, cin, cout, BT, hh, ww):
     x = rnd(BT, cin, hh, ww, seed=15)
     w = rnd(cin, cout, k, k, scale=cin ** -0.5, seed=16)

@@ -742,7 +742,12 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
   static_assert(EK != 3 || (ACT == VDA_ACT_NONE && LNF), "EK 3: LN fold + per-frame row bias, no activation");
   const bool has_bias = EK ? true : p.epi.bias != nullptr;
   const bool has_gamma = EK ? false : p.epi.gamma != nullptr;
-  const bool rows_store = EK ? true : p.epi.store == VDA_STORE_ROWS;
+  // ConvTranspose(k = s) pixel-shuffle stores through the staged row epilogue when a 256-wide N tile is
+  // 256 consecutive channels of ONE output pixel (cout % 256 == 0): its rows are then whole 512-B output
+  // pixel runs at remapped addresses (phase 2 below), instead of 8-byte scatter stores per element
+  const bool ps_rows = !EK && ACT != VDA_ACT_GEGLU && !ROWB && XR == 2 && p.epi.store == VDA_STORE_PIXEL_SHUFFLE &&
+                       p.epi.ps_cout % 256 == 0 && p.epi.ps_win >= 16 && (long)p.M * p.N * 2 < 0x7fffffffL;
+  const bool rows_store = EK ? true : (p.epi.store == VDA_STORE_ROWS || ps_rows);
   const bool has_res = EK == 2 ? true : (EK == 1 || EK == 3) ? false : p.epi.res != nullptr;
   const bool has_res2 = EK ? false : p.epi.res2 != nullptr;
   const bool has_stats = EK == 2 ? true : (EK == 1 || EK == 3) ? false : p.epi.stats_out != nullptr;
@@ -1642,7 +1647,36 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
       const unsigned vo = m < p.M ? (unsigned)((((long)m * P + (n0 >> 8)) * 2 + ((lane >> 4) & 1)) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, r), rs, vo, 0, 0);
     };
-    if (nres == 0) {
+    // pixel shuffle (ps_rows): tile row m = input pixel (bt, yh, xw), its 256 columns = channels co0 ..
+    // co0 + 255 of output pixel (yh k + ki, xw k + kj); the row walk advances (xw, yh, bt) incrementally
+    // (RPI = 16 rows per step, ps_win >= 16: at most one wrap)
+    auto ps_store = [&]() {
+      if constexpr (RPI == 16 && ACT != VDA_ACT_GEGLU && !ROWB && XR == 2) {  // the instantiations ps_rows admits
+      const int k = e.ps_k, cout = e.ps_cout, win = e.ps_win, hin = e.ps_hin;
+      const int ij = n0 / cout, co0 = n0 - ij * cout, ki = ij / k, kj = ij - ki * k;
+      const __amdgpu_buffer_rsrc_t rz =
+          __builtin_amdgcn_make_buffer_rsrc((void*)p.y, (short)0, (int)((long)p.M * p.N * 2), 0x00020000);
+      int m = m0 + row0;
+      int xw = m % win, tq = m / win;
+      int yh = tq % hin, bt = tq / hin;
+      const long rowlen = (long)win * k;
+#pragma unroll
+      for (int it = 0; it < NIT; ++it) {
+        const long pix = ((long)(bt * hin + yh) * k + ki) * rowlen + (long)xw * k + kj;
+        const unsigned off = m < p.M ? (unsigned)((pix * cout + co0 + q * 8) * 2) : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tv[it]), rz, off, 0, VDA_EPI_STORE_AUX);
+        m += RPI;
+        xw += RPI;
+        if (xw >= win) {
+          xw -= win;
+          if (++yh == hin) { yh = 0; ++bt; }
+        }
+      }
+      }
+    };
+    if (ps_rows) {
+      ps_store();
+    } else if (nres == 0) {
       if constexpr (RPF) {
         if (has_stats) store_with_stats(std::false_type{});
         else phase2(std::integral_constant<int, 0>{});
