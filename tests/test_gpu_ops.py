@@ -902,3 +902,15 @@ def test_gemm_dynamic_tile_schedule(M, N, K, kind):
     assert all(int(c.abs().sum()) == 0 for c in cs)
     # the model's per-stream counter sets
     assert ops.sched_counters().dtype == torch.int32 and ops.sched_counters() is ops.sched_counters()
+
+
+@pytest.mark.parametrize("BT,H,W", [(2, 70, 518), (3, 28, 924), (1, 14, 1036)])
+def test_patch_im2col_exact(BT, H, W):
+    """patch_embed.py:69-82 input: the [BT, 1 + np, Kp] fp16 patch matrix is the exact fp16 of the
+    image's 14 x 14 patches (channel-major: k = c * 196 + ky * 14 + kx), zero cls rows and zero K padding."""
+    img = rnd(BT, 3, H, W, seed=45)
+    a = ops.patch_im2col(img.to(DEV).contiguous(), 640).cpu()
+    np_ = (H // 14) * (W // 14)
+    ref = torch.zeros(BT, np_ + 1, 640, dtype=torch.float16)
+    ref[:, 1:, :588] = F.unfold(img, 14, stride=14).transpose(1, 2).half()
+    assert torch.equal(a.view(BT, np_ + 1, 640), ref)

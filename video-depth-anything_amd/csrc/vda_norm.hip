@@ -209,14 +209,16 @@ __global__ __launch_bounds__(256) void groupnorm_kernel(const h16* __restrict__ 
 }
 
 // GroupNorm, three coalesced passes over [F, S, C] (used when the caller passes a workspace):
-//   gn_partial:  block (frame, chunk of GN_ROWS rows) reads whole rows (16 B per thread) and writes
+//   gn_partial:  block (frame, chunk of gn_rows(C) rows) reads whole rows (16 B per thread) and writes
 //                per-channel partial sums of d and d^2, d = x - shift_g (shift_g = the group's first
 //                value of the frame, so the one-pass variance does not cancel);
 //   gn_finalize: per (frame, group) mean and rstd from the partials, fixed summation order;
 //   gn_apply:    y = (x - mean) * rstd * gamma + beta, same row-chunk grid.
 // Deterministic (no atomics).  The per-(frame, group) kernel above reads strided 16-B slivers of
 // every row three times; these read each row once per pass with full-row coalescing.
-constexpr int GN_ROWS = 128;
+// Rows per (frame, chunk) block: 128, or 32 for C >= 512 (there 128 rows are 64 sequential loads per
+// thread and a 19^2 map gave 96 blocks for 256 CUs: 34.7 us for 24 MB, round 4's forward trace)
+__host__ __device__ constexpr int gn_rows(int C) { return C >= 512 ? 32 : 128; }
 
 __device__ __forceinline__ void gn_layout(int C, int& cpr, int& rpi) {
   cpr = C >> 3;          // 8-channel chunks per row
@@ -241,8 +243,9 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__
     s2[j] = 0.f;
   }
   if (r0 < rpi) {
-    const int rend = min(S, (ch + 1) * GN_ROWS);
-    for (int r = ch * GN_ROWS + r0; r < rend; r += rpi) {
+    const int rend = min(S, (ch + 1) * gn_rows(C));
+#pragma unroll 4
+    for (int r = ch * gn_rows(C) + r0; r < rend; r += rpi) {
       const h8 v = __builtin_bit_cast(h8, ldg16(fx + (long)r * C + cc * 8));
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -317,8 +320,9 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x
     of[j] = bet[c] - mean * sc[j];
   }
   const long fo = (long)f * S * C;
-  const int rend = min(S, (ch + 1) * GN_ROWS);
-  for (int r = ch * GN_ROWS + r0; r < rend; r += rpi) {
+  const int rend = min(S, (ch + 1) * gn_rows(C));
+#pragma unroll 4
+  for (int r = ch * gn_rows(C) + r0; r < rend; r += rpi) {
     const h8 v = __builtin_bit_cast(h8, ldg16(x + fo + (long)r * C + cc * 8));
     h8 o;
 #pragma unroll
@@ -381,7 +385,7 @@ extern "C" int vda_layernorm(const void* x, int64_t ldx, void* y, const float* g
 
 extern "C" int64_t vda_groupnorm_workspace(int32_t F, int32_t S, int32_t C, int32_t groups) {
   if (F <= 0 || S <= 0 || C <= 0 || groups <= 0) return 0;
-  const long nchunk = (S + GN_ROWS - 1) / GN_ROWS;
+  const long nchunk = (S + gn_rows(C) - 1) / gn_rows(C);
   return (int64_t)(2L * F * nchunk * C + 2L * F * groups);
 }
 
@@ -393,7 +397,7 @@ extern "C" int vda_groupnorm(const void* x, void* y, const float* gamma, const f
   VDA_CHECK_ARG(cg % 2 == 0, "channels per group must be even");
   hipStream_t st = (hipStream_t)stream;
   if (ws && C % 8 == 0 && C <= 2048) {
-    const int nchunk = (S + GN_ROWS - 1) / GN_ROWS;
+    const int nchunk = (S + gn_rows(C) - 1) / gn_rows(C);
     float* stats = ws + 2L * F * nchunk * C;
     hipLaunchKernelGGL(gn_partial_kernel, dim3(F * nchunk), dim3(256), 0, st, (const h16*)x, ws, S, C, groups, nchunk);
     hipLaunchKernelGGL(gn_finalize_kernel, dim3(F * groups), dim3(64), 0, st, (const h16*)x, (const float*)ws, stats, S,
