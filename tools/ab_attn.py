@@ -1,6 +1,7 @@
 """In-process A/B of the spatial attention across libvda builds (tuning tool, not product code).
 
-usage: python tools/ab_attn.py LIB_A.so [LIB_B.so ...] [--rounds R]
+usage: python tools/ab_attn.py LIB_A.so[@K] [LIB_B.so[@K] ...] [--rounds R]
+(@K: a tuning-build library with vda_debug_attn(K, 0) set, e.g. build/tune/libvda.so@2 = the v2 kernel)
 ViT-L clip shape (32 frames x 1370 tokens x 16 heads x 64) through the C ABI (vda_spatial_attention)
 on the current torch stream; rounds alternate the libraries; outputs compared bit-for-bit against the
 first library's and (first 2 frames) against torch SDPA in fp32.
@@ -26,8 +27,11 @@ while i < len(args):
         libs.append(args[i]); i += 1
 L = []
 for p in libs:
-    l = ctypes.CDLL(os.path.abspath(p))
+    path, _, knob = p.partition("@")
+    l = ctypes.CDLL(os.path.abspath(path))
     _lib._declare(l)
+    if knob:
+        assert l.vda_debug_attn(int(knob), 0) == 0
     L.append(l)
 B, N, H, D = 32, 1370, 16, 64
 torch.manual_seed(0)
