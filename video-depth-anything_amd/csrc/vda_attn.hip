@@ -223,7 +223,9 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 // issuing the QK MFMAs of tile t+1 before the softmax of tile t (213 VGPRs, a 4-slot ring, two blocks
 // per CU) 333 vs 292 us; with the per-tile max still computed, 354 vs 320 us; each 32-key half of a
 // tile exponentiated, checked and multiplied into O on its own (so half 0's softmax can sit beside
-// half 1's QK MFMAs): 302 vs 297 us.
+// half 1's QK MFMAs): 302 vs 297 us.  Round 5: two 32-query sets per wave (every K / Vᵀ fragment read
+// feeds two MFMAs; 251 VGPRs, two blocks of 4 x 64 queries per CU, 4-deep ring), with set B half a tile
+// behind set A or in plain order: 317.8 / 307.8 vs 275.0 us, bit-identical (r05_ab_attn_two_sets.log).
 // =============================================================================================
 constexpr int SA_KT = 64;    // keys per tile
 constexpr int SA_QB = 128;   // queries per block
@@ -425,247 +427,6 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
         for (int r = 0; r < 4; ++r) v[r] = (h16)(o[dt][gq * 4 + r] * inv);
         *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
       }
-  }
-}
-
-// =============================================================================================
-// Spatial attention v3, D = 64: the v2 kernel above with TWO 32-query column sets per wave (A = queries
-// q0 .. q0+31, B = q0+32 .. q0+63), so every K fragment (ds_read_b128) and every transposed V fragment
-// (2 x ds_read_b64_tr_b16) feeds two MFMAs, and the two sets' chains are independent work for one wave
-// to interleave.  Block = 4 waves x 64 queries = 256 queries of one (batch, head), two blocks per CU
-// (<= 256 VGPRs, 64 KiB of LDS each).  Set B runs half a tile behind set A: per key tile t the MFMA
-// stream is  QK_A(t) | PV_B(t-1) | QK_B(t) | PV_A(t)  and each set's softmax (exp2 / row sum / fp16
-// pack) sits beside the other set's MFMAs.  PV_B(t-1) still reads tile t-1's V, so the K/V ring is 4
-// deep (tile t+2 streams into the slot of tile t-2).  Per set the math is the v2 kernel's: scores
-// relative to the running reference m (chain started from C = -m), deferred re-base when a lane's
-// tile P sum passes 2^15, the same fp32 sums and fp16 P, so the output matches v2's bit for bit.
-// =============================================================================================
-constexpr int SA3_QB = 256;   // queries per block
-constexpr int SA3_NBUF = 4;   // K/V ring depth
-
-template <int SKEW>
-__global__ __launch_bounds__(256, 2) void spatial_attn64_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                                int N, int H, int nqb, int nblocks, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) h16 sKV[SA3_NBUF][2][SA_KT * SD];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  int id = blockIdx.x;
-  const int per = nblocks >> 3;
-  if (id < per * 8) id = (id & 7) * per + (id >> 3);
-  const int qb = __builtin_amdgcn_readfirstlane(id % nqb), bh = id / nqb;
-  const int h = __builtin_amdgcn_readfirstlane(bh % H), b = __builtin_amdgcn_readfirstlane(bh / H);
-  const int C = H * SD;
-  const long ld = 3L * C;
-  const h16* base = qkv + (long)b * N * ld + h * SD;
-  const int r32 = lane & 31, hf = lane >> 5;
-  const int q0 = qb * SA3_QB + wave * 64;  // wave-uniform: a wave past N only moves its K/V pieces
-  const bool active = q0 < N;
-
-  h8 qf[2][4];
-#pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int q = q0 + s * 32 + r32;
-      h8 t = h8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (q < N) t = __builtin_bit_cast(h8, ldg16(base + (long)q * ld + ks * 16 + hf * 8));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) t[e] = (h16)((float)t[e] * scale_log2);
-      qf[s][ks] = t;
-    }
-
-  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
-  unsigned voff[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
-    const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
-    const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
-    voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
-  }
-  auto dma = [&](int kt) {
-    const int buf = kt % SA3_NBUF;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
-                                               (int)(kt * SA_KT * ld * 2), 0, 0);
-    }
-  };
-
-  f16x o[2][2] = {{f16x{}, f16x{}}, {f16x{}, f16x{}}};
-  f16x negm[2] = {f16x{}, f16x{}};
-  float mrun[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
-  const int grp = lane >> 4, li = lane & 15, q4 = li >> 2, p4 = li & 3;
-  unsigned kofs[4], vofs[2];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) kofs[ks] = (unsigned)sa_kslot(r32, ks * 2 + hf) * 16u;
-#pragma unroll
-  for (int dt = 0; dt < 2; ++dt) {
-    const int col = dt * 32 + (grp & 1) * 16 + 4 * p4, r0 = 4 * (grp >> 1) + q4;
-    vofs[dt] = (unsigned)(sa_vslot(r0, col >> 3) * 8 + (col & 7)) * 2u;
-  }
-  auto slot_base = [&](int kt) {  // ring slot byte offset (opaque, see the v2 kernel)
-    unsigned bo;
-    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % SA3_NBUF), "n"(2 * SA_KT * SD * 2));
-    return reinterpret_cast<const char*>(sKV[0][0]) + bo;
-  };
-  f16x sc[2][2];
-  h8 pf[2][4];
-  auto qk = [&](auto set_tag, const char* kbase, int kt, bool mask) {
-    constexpr int S = decltype(set_tag)::value;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
-        sc[S][kb] = mfma32(kf, qf[S][ks], ks == 0 ? negm[S] : sc[S][kb]);
-      }
-    if (mask) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) sc[S][kb][r] = -INFINITY;
-    }
-  };
-  auto tile_max = [&](auto set_tag) {
-    constexpr int S = decltype(set_tag)::value;
-    float mx = fmaxf(fmaxf(sc[S][0][0], sc[S][0][1]), sc[S][0][2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[S][0][r]), sc[S][0][r + 1]);
-    mx = fmaxf(fmaxf(mx, sc[S][0][15]), sc[S][1][0]);
-#pragma unroll
-    for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[S][1][r]), sc[S][1][r + 1]);
-    mx = fmaxf(mx, sc[S][1][15]);
-    return half_max(mx);
-  };
-  auto rebase = [&](auto set_tag, float sh) {
-    constexpr int S = decltype(set_tag)::value;
-    mrun[S] += sh;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) negm[S][r] = -mrun[S];
-    sc[S][0] -= sh;
-    sc[S][1] -= sh;
-  };
-  auto expo = [&](auto set_tag, float& t0, float& t1) {
-    constexpr int S = decltype(set_tag)::value;
-    t0 = 0.f;
-    t1 = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float pv = __builtin_amdgcn_exp2f(sc[S][kb][r]);
-        if (kb == 0) t0 += pv;
-        else t1 += pv;
-        pf[S][kb * 2 + (r >> 3)][r & 7] = (h16)pv;
-      }
-  };
-  // softmax of one set's tile: FIRST re-bases on the true tile max, later tiles only when the P sum
-  // passes 2^15 (then the scores are recomputed from the still-resident K slot, as in v2)
-  auto soft = [&](auto set_tag, auto first_tag, const char* kbase, int kt, bool mask) {
-    constexpr int S = decltype(set_tag)::value;
-    float t0, t1;
-    if constexpr (decltype(first_tag)::value) {
-      rebase(set_tag, tile_max(set_tag));
-      expo(set_tag, t0, t1);
-    } else {
-      expo(set_tag, t0, t1);
-      if (__any(!(t0 + t1 <= 32768.f))) {
-        qk(set_tag, kbase, kt, mask);
-        const float sh = fmaxf(tile_max(set_tag), 0.f);
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-        lsum[S] *= alpha;
-        o[S][0] *= alpha;
-        o[S][1] *= alpha;
-        rebase(set_tag, sh);
-        expo(set_tag, t0, t1);
-      }
-    }
-    lsum[S] += t0 + t1;
-  };
-  auto pv = [&](auto set_tag, const char* vbase) {
-    constexpr int S = decltype(set_tag)::value;
-#pragma unroll
-    for (int ps = 0; ps < 4; ++ps)
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const char* va = vbase + vofs[dt] + ps * 2048;
-        const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
-        const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
-        const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        o[S][dt] = mfma32(vf, pf[S][ps], o[S][dt]);
-      }
-  };
-  using SA = std::integral_constant<int, 0>;
-  using SB = std::integral_constant<int, 1>;
-  constexpr int KV = SA_KT * SD * 2;  // byte offset of a slot's V image from its K image
-
-  const int ntiles = (N + SA_KT - 1) / SA_KT;
-  const bool tail = N % SA_KT != 0;
-  auto enter = [&](int kt) {  // tile kt landed and visible; slot of kt-2 free -> prefetch kt+2
-    if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (kt + 2 < ntiles) dma(kt + 2);
-  };
-  dma(0);
-  if (ntiles > 1) dma(1);
-  enter(0);
-  if (active) {
-    const char* kb0 = slot_base(0);
-    const bool m0 = tail && ntiles == 1;
-    qk(SA{}, kb0, 0, m0);
-    soft(SA{}, std::true_type{}, kb0, 0, m0);
-    qk(SB{}, kb0, 0, m0);
-    pv(SA{}, kb0 + KV);
-    soft(SB{}, std::true_type{}, kb0, 0, m0);
-    if constexpr (!SKEW) pv(SB{}, kb0 + KV);
-  }
-  for (int kt = 1; kt < ntiles; ++kt) {
-    enter(kt);
-    if (active) {
-      const char* kb = slot_base(kt);
-      const char* kp = slot_base(kt - 1);
-      const bool m = tail && kt == ntiles - 1;
-      if constexpr (SKEW) {
-        qk(SA{}, kb, kt, m);
-        pv(SB{}, kp + KV);
-        soft(SA{}, std::false_type{}, kb, kt, m);
-        qk(SB{}, kb, kt, m);
-        pv(SA{}, kb + KV);
-        soft(SB{}, std::false_type{}, kb, kt, m);
-      } else {
-        (void)kp;
-        qk(SA{}, kb, kt, m);
-        qk(SB{}, kb, kt, m);
-        soft(SA{}, std::false_type{}, kb, kt, m);
-        pv(SA{}, kb + KV);
-        soft(SB{}, std::false_type{}, kb, kt, m);
-        pv(SB{}, kb + KV);
-      }
-    }
-  }
-  if (active) {
-    if constexpr (SKEW) pv(SB{}, slot_base(ntiles - 1) + KV);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float inv = 1.f / half_sum(lsum[s]);
-      const int q = q0 + s * 32 + r32;
-      if (q < N) {
-        h16* op = out + ((long)b * N + q) * C + h * SD;
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq) {
-            h4 v;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = (h16)(o[s][dt][gq * 4 + r] * inv);
-            *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
-          }
-      }
-    }
   }
 }
 
@@ -916,18 +677,15 @@ __global__ __launch_bounds__(64 * NW) void temporal_attn_lds_kernel(const h16* _
   }
 }
 
-// vda_debug_attn (tuning build): spatial 1 = the round-1 kernel, 2 = the one-set-per-wave v2 kernel;
-// temporal 1 = the direct-load kernel
+// vda_debug_attn (tuning build): the round-1 spatial kernel / the direct-load temporal kernel
 VDA_KNOB(int, g_sa_old, 0);
-VDA_KNOB(int, g_sa_v2, 0);
 VDA_KNOB(int, g_ta_old, 0);
 
 }  // namespace
 
 #ifdef VDA_TUNING
 extern "C" int vda_debug_attn(int32_t spatial_old, int32_t temporal_old) {
-  g_sa_old = spatial_old == 1;
-  g_sa_v2 = spatial_old >= 2 ? spatial_old : 0;
+  g_sa_old = spatial_old;
   g_ta_old = temporal_old;
   return 0;
 }
@@ -942,21 +700,11 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
     dim3 grid((N + SQB - 1) / SQB, H, B);
     hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, scale * 1.4426950408889634f);
-  } else if (g_sa_v2 == 2) {
+  } else {
     const int nqb = (N + SA_QB - 1) / SA_QB;
     const long nb = (long)nqb * H * B;
     VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
     hipLaunchKernelGGL(spatial_attn32_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
-                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
-  } else {
-    const int nqb = (N + SA3_QB - 1) / SA3_QB;
-    const long nb = (long)nqb * H * B;
-    VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
-    if (g_sa_v2 == 3)
-      hipLaunchKernelGGL(spatial_attn64_kernel<0>, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
-                         (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
-    else
-    hipLaunchKernelGGL(spatial_attn64_kernel<1>, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
   }
   VDA_LAUNCH_CHECK();
