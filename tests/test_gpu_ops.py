@@ -512,11 +512,13 @@ def test_depth_head_fused_resize(C, Hin, Win, Ho, Wo, BT):
 
 
 @pytest.mark.parametrize("BT,Cin,Hs,Ws,H,W,relu", [(2, 256, 70, 70, 140, 140, False), (2, 128, 64, 72, 128, 143, True),
-                                                   (1, 64, 20, 150, 39, 299, False), (3, 128, 9, 9, 17, 17, False)])
+                                                   (1, 64, 20, 150, 39, 299, False), (3, 128, 9, 9, 17, 17, False),
+                                                   (4, 128, 148, 148, 296, 296, True)])
 def test_conv3x3_halo_fused_resize(BT, Cin, Hs, Ws, H, W, relu):
     """output_conv1 shape class (3x3, Cout = 128) on a bilinear align_corners=True resize fused into the
     halo conv's patch staging: vs torch fp32, and bit-identical to resize + halo conv when the
-    materialised path also takes the halo kernel (resized maps >= 128^2)."""
+    materialised path also takes the halo kernel (resized maps >= 128^2).  4 x 296^2: more tiles than CUs,
+    so the interpolation waves build the next unit's patch across tile boundaries."""
     x = rnd(BT, Cin, Hs, Ws, seed=170)
     w = rnd(128, Cin, 3, 3, scale=(9 * Cin) ** -0.5, seed=171)
     b = rnd(128, scale=0.1, seed=172)

@@ -37,7 +37,6 @@ constexpr int DC_PSLOT = DC_PP * 512;           // halfs
 constexpr int DC_WROW = 3 * 64 * 32;            // halfs of one phase's W (3 taps x 64 rows x 32 channels)
 constexpr int DC_SRCP = 12;                     // UPS: 1-KiB pieces of the source-region slot (192 pixels)
 constexpr int DC_SSLOT = DC_SRCP * 512;         // halfs
-constexpr int DC_IT = (DC_NPIX * 4 + 255) / 256;  // UPS: interpolated patch slots per thread (6)
 
 
 template <int N>
@@ -62,7 +61,7 @@ __device__ __forceinline__ void dc_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F);
 
 // UPS: U is the map BEFORE the bilinear (align_corners=True) resize from (Hs, Ws) to (H, W); each
 // unit's patch is interpolated in LDS from a staged source region (bilerp8, the resize kernel's
-// formula: bit-identical to resize + conv) by the block's own waves after their MFMAs of the unit's
+// formula, separably: bit-identical to resize + conv) by the block's own waves after their MFMAs of the unit's
 // middle row, while the other block of the CU keeps the matrix cores busy.  W then uses a 2-slot ring
 // (one phase ahead) to make room for the 12-KiB source slot.
 #ifdef VDA_TS  // per-block phase-class cycle sums of the fused depth conv (tools/ts_dconv.py; experiments only)
@@ -172,40 +171,72 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (VDA_LDS void*)(ssm + q * 512), 16, (int)vo, slab * 64, 0, 0);
     }
   };
-  // interpolate unit u's patch from the source slot into patch slot (u & 1); padding pixels -> 0.
-  // Thread slot s = tid + 256 it: pixel s >> 2, LDS position s & 3 holding chunk (s & 3) ^ ((p >> 1) & 3)
-  auto interp = [&](int u, int it0, int it1) {
+  // interpolate unit u's patch from the source slot into patch slot (u & 1) (padding pixels -> 0),
+  // separably: bilerp8_mix's blend is o = fma(wy, bot, uy * top) with top / bot the horizontal blends
+  // fma(wx, B, ux * A) of source rows sy0 / sy1 at the output column, and a source row's horizontal
+  // blend at a column does not depend on the output row that uses it, so each is formed once per
+  // (column, source row) and carried down the column: the same ops, bit-identical to bilerp8_mix per
+  // pixel (and so to vda_upsample_bilinear), in ~45 % of its VALU.
+  // Thread = (column px_l, channel chunk c, 6-row segment): waves 0..2 own columns 0..15 of segment
+  // `wave` (the row, hence sy0 / sy1 / wy, is wave-uniform), lanes 0..23 of wave 3 columns 16, 17.
+  auto interp_sep = [&](int u) {
     int bt, y0, x0, sy_lo, sx_lo, SR, SC;
     tile_of(u / nslab, bt, y0, x0);
     src_region(y0, x0, sy_lo, sx_lo, SR, SC);
     (void)bt; (void)SR;
+    const bool w3 = wave == 3;
+    const int seg = w3 ? lane >> 3 : wave;
+    const int px_l = w3 ? 16 + ((lane >> 2) & 1) : lane >> 2, c = lane & 3;
+    if (w3 && lane >= 24) return;
+    const int pxg = x0 - 1 + px_l;
+    const bool okx = (unsigned)pxg < (unsigned)W;
+    const float ox = (float)min(max(pxg, 0), W - 1);
+    const int sx0 = (int)(usx * ox), sx1 = min(sx0 + 1, Ws - 1);
+    const float wx = ac_weight(usx, ox, sx0), ux = 1.f - wx;
+    const int c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
+    auto hrow = [&](int sy, float (&t)[8]) {
+      const int r = (sy - sy_lo) * SC;
+      const uint4 a = *reinterpret_cast<const uint4*>(ssm + ((r + c0) * 4 + c) * 8);
+      const uint4 b = *reinterpret_cast<const uint4*>(ssm + ((r + c1) * 4 + c) * 8);
+      const unsigned A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
 #pragma unroll
-    for (int it = it0; it < it1; ++it) {
-      const int sl = tid + 256 * it;
-      if (sl < DC_NPIX * 4) {
-        const int p = sl >> 2;
-        const int cd = (sl & 3) ^ ((p >> 1) & 3);
-        const int pr = p / DC_P;
-        const int py = y0 - 1 + pr, px = x0 - 1 + (p - pr * DC_P);
-        const bool ok = (unsigned)py < (unsigned)H && (unsigned)px < (unsigned)W;
-        int sy0, sy1, sx0, sx1;
-        float wy, wx;
-        {
-          const float oy = (float)min(max(py, 0), H - 1), ox = (float)min(max(px, 0), W - 1);
-          const float fy = usy * oy;
-          sy0 = (int)fy; sy1 = min(sy0 + 1, Hs - 1); wy = ac_weight(usy, oy, sy0);
-          const float fx = usx * ox;
-          sx0 = (int)fx; sx1 = min(sx0 + 1, Ws - 1); wx = ac_weight(usx, ox, sx0);
-        }
-        const int r0 = (sy0 - sy_lo) * SC, r1 = (sy1 - sy_lo) * SC, c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
-        const uint4 a = *reinterpret_cast<const uint4*>(ssm + ((r0 + c0) * 4 + cd) * 8);
-        const uint4 b = *reinterpret_cast<const uint4*>(ssm + ((r0 + c1) * 4 + cd) * 8);
-        const uint4 c = *reinterpret_cast<const uint4*>(ssm + ((r1 + c0) * 4 + cd) * 8);
-        const uint4 d = *reinterpret_cast<const uint4*>(ssm + ((r1 + c1) * 4 + cd) * 8);
-        const uint4 v = bilerp8_mix(a, b, c, d, wx, wy);
-        const uint4 o = ok ? v : make_uint4(0u, 0u, 0u, 0u);
-        *reinterpret_cast<uint4*>(psm + (u & 1) * DC_PSLOT + sl * 8) = o;
+      for (int j = 0; j < 4; ++j) {
+        t[2 * j] = fma_mix_lo(wx, B[j], fma_mix_lo(ux, A[j], -0.f));
+        t[2 * j + 1] = fma_mix_hi(wx, B[j], fma_mix_hi(ux, A[j], -0.f));
       }
+    };
+    float top[8], bot[8];
+    int s0 = -1, s1 = -1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int pr = seg * 6 + k;
+      const int pyg = y0 - 1 + pr;
+      const float oy = (float)min(max(pyg, 0), H - 1);
+      const int sy0 = (int)(usy * oy), sy1 = min(sy0 + 1, Hs - 1);
+      const float wy = ac_weight(usy, oy, sy0), uy = 1.f - wy;
+      if (sy0 != s0) {  // scale <= 1: the source rows advance by at most one per output row
+        if (sy0 == s1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) top[e] = bot[e];
+        } else {
+          hrow(sy0, top);
+        }
+        hrow(sy1, bot);
+        s0 = sy0;
+        s1 = sy1;
+      }
+      unsigned o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float ol = fma_f32(wy, bot[2 * j], mul_f32(uy, top[2 * j]));
+        const float oh = fma_f32(wy, bot[2 * j + 1], mul_f32(uy, top[2 * j + 1]));
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        o[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{ol, oh}, h2));
+      }
+      const bool ok = okx && (unsigned)pyg < (unsigned)H;
+      const uint4 v = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
+      const int p = pr * DC_P + px_l;
+      *reinterpret_cast<uint4*>(psm + (u & 1) * DC_PSLOT + (p * 4 + (c ^ ((p >> 1) & 3))) * 8) = v;
     }
   };
   // this wave's 3 pieces of phase g's W slice (kernel row dy = g % 3 of unit g / 3) -> slot g % 3
@@ -231,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
     w_dma(0);
     dc_wait<0>();
     __builtin_amdgcn_s_barrier();
-    interp(0, 0, DC_IT);
+    interp_sep(0);
     dc_lgkm0();
     __builtin_amdgcn_s_barrier();
     if (my_units > 1) src_dma(1);
@@ -317,7 +348,7 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
     const bool wnext = g + (UPS ? 1 : 2) < G;
     if (wnext) w_dma(g + (UPS ? 1 : 2));
     if constexpr (UPS) {
-      if (dy == 2 && u + 2 < my_units) src_dma(u + 2);  // the source slot interp(u + 1) read in row 1
+      if (dy == 2 && u + 2 < my_units) src_dma(u + 2);  // the source slot interp_sep(u + 1) read in row 1
     } else {
       if (dy == 0 && u + 1 < my_units) patch_dma(u + 1);
     }
@@ -376,7 +407,7 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
       // by the row-0 wait), writes complete before barrier g + 1 (a 3 + 3 split over rows 1 and 2,
       // with the source staged in row 0, measured 3 % slower: the source fetch then has one phase)
       if (dy == 1 && u + 1 < my_units) {
-        interp(u + 1, 0, DC_IT);
+        interp_sep(u + 1);
         dc_lgkm0();
       }
       // W(g + 1) (issued this phase) must have landed before barrier g + 1; so must, at row 0, the

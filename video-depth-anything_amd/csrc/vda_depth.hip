@@ -72,8 +72,12 @@ __device__ __forceinline__ void dh_ac_coord(int o, int in, float sc, int& i0, in
 // filled at a unit's first step and consumed at its last), and at the unit's last step every thread
 // interpolates its 16-B patch slots from LDS in fp32 (bilerp8: the resize kernel's formula and
 // op order, so the fp16 values are bit-identical) into the other patch ring slot.
-template <int SLAB, int NROW, int TPS, bool DEPTH, bool UPS = false>
-__global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
+// IW (UPS only): IW extra interpolation waves (8 .. 8+IW-1) own the source staging and the
+// interpolation: they fetch unit u+1's source region at step 0 of unit u and build its patch over steps
+// 2 .. 7 (512 slots a step), beside the 8 MFMA waves' taps, which then never stop for the
+// interpolation; every wave takes every step barrier.
+template <int SLAB, int NROW, int TPS, bool DEPTH, bool UPS = false, int IW = 0>
+__global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ w2,
                                                         const float* __restrict__ b2, float* __restrict__ depth,
                                                         h16* __restrict__ yout, int relu_out,
@@ -100,6 +104,7 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   constexpr int ND = SLAB / 32;                          // MFMA k-depths per tap
   constexpr int WRING = 2;                               // weight ring
   static_assert(!UPS || 9 / TPS >= 2, "UPS: >= 2 steps per unit");
+  static_assert(IW == 0 || (UPS && TPS == 1), "interpolation waves: the 9-step fused-resize conv");
   constexpr int SPPW = (192 * CPX + 511) / 512;          // UPS source pieces per wave (fixed count)
   constexpr int SSLOT = UPS ? SPPW * 8 * 64 : 0;         // source slots: >= 192 pixels x CPX chunks
   __shared__ __attribute__((aligned(16))) h16 dsm[2 * PBUF + WRING * WBUF + SSLOT * 8 + 512];
@@ -111,6 +116,7 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int mg = wave & 3, ng = wave >> 2;
+  const bool iwave = IW > 0 && wave >= 8;                // interpolation wave (no MFMA work)
   const int nslab = C / SLAB;
   const int K = 9 * C;
   const int units_per_tile = nslab;
@@ -166,9 +172,8 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     return ud;
   };
   // piece j (of SPPW) of unit u's source region -> sbuf; slot = pixel * CPX + chunk
-  auto dma_src = [&](const Ud& ud, int j) {
+  auto dma_src = [&](const Ud& ud, int q) {
     const int bt = ud.bt, sy_lo = ud.sy_lo, sx_lo = ud.sx_lo, SR = ud.SR, SC = ud.SC, slab = ud.slab;
-    const int q = wave + j * 8;
     const int s = q * 64 + lane;
     const int px = s / CPX, cd = s % CPX;
     const int r = px / SC, c = px - r * SC;
@@ -177,11 +182,13 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     dh_glds16(src, sbuf + q * 512);
   };
   // interpolate unit u's patch from sbuf into patch ring slot (u & 1); padding pixels -> 0
-  auto ups_interp = [&](int u, const Ud& ud) {
+  // slots t0 + k * tstride (k < NK) of the patch (t0 = this thread's first)
+  auto ups_interp = [&](int u, const Ud& ud, int t0, int tstride, auto nk_tag) {
+    constexpr int NK = decltype(nk_tag)::value;
     const int y0 = ud.y0, x0 = ud.x0, sy_lo = ud.sy_lo, sx_lo = ud.sx_lo, SC = ud.SC;
 #pragma unroll
-    for (int k = 0; k < UCH; ++k) {
-      const int s = tid + k * 512;
+    for (int k = 0; k < NK; ++k) {
+      const int s = t0 + k * tstride;
       const int sc = min(s, USL - 1);
       const int p = sc / CPX, pos = sc - p * CPX;
       const int cd = LIN ? pos : patch_pos<CPX>(p, pos);
@@ -203,7 +210,7 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       const int slot = LIN ? p * PSTR + pos : s;
       // asm store: a compiler-visible LDS store that may alias the LDS-DMA ring gets an s_waitcnt
       // vmcnt(0) in front of it, which drained the next step's weight DMA before the interpolation
-      if (k + 1 < UCH || s < USL)
+      if (s < USL)
         asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)(VDA_LDS h16*)(patch + (u & 1) * PBUF + slot * 8)),
                      "v"(__builtin_bit_cast(dh_u4, o))
                      : "memory");
@@ -226,11 +233,13 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   // prologue: patch of unit 0 (all pieces, split over waves) + weights of step 0
   Ud ud_next = make_ud(0);
   if constexpr (UPS) {
-    for (int j = 0; j < SPPW; ++j) dma_src(ud_next, j);
-    dma_w(0, ud_next.slab, 0);
+    if (!iwave) {
+      for (int j = 0; j < SPPW; ++j) dma_src(ud_next, wave + j * 8);
+      dma_w(0, ud_next.slab, 0);
+    }
     dh_wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
-    ups_interp(0, ud_next);
+    if (!iwave) ups_interp(0, ud_next, tid, 512, std::integral_constant<int, UCH>{});
     __syncthreads();  // patch slot 0 written, source slot free for unit 1
   } else {
     for (int q = wave; q < PP; q += 8) dma_patch(0, ud_next, q);
@@ -239,6 +248,31 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
   }
   __builtin_amdgcn_s_barrier();
 
+  if constexpr (IW > 0) {
+    if (iwave) {
+      // the interpolation waves' own step loop (same barrier sequence as the MFMA waves' loop below, no
+      // accumulators live): unit u+1's source region at step 0 (waited for before step 1's barrier),
+      // its patch over steps 2 .. 7; the step barriers publish the writes (lgkmcnt(0) in ups_interp)
+      constexpr int SPI = SPPW * 8 / IW;                 // source pieces per interpolation wave
+      static_assert(SPPW * 8 % IW == 0 && 6 * 128 * IW >= USL, "interpolation wave split");
+      int iu = 0, ist = 0;
+      for (int gs = 0; gs < my_steps; ++gs) {
+        if (ist == 0 && iu + 1 < my_units) {
+          ud_next = make_ud(iu + 1);
+          for (int j = 0; j < SPI; ++j) dma_src(ud_next, (wave - 8) + j * IW);
+        }
+        if (ist >= 2 && ist < 8 && iu + 1 < my_units)
+          ups_interp(iu + 1, ud_next, (ist - 2) * 128 * IW + (tid - 512), 64 * IW, std::integral_constant<int, 2>{});
+        if (ist == 1) dh_wait_vmcnt<0>();
+        __builtin_amdgcn_s_barrier();
+        if (++ist == SPU) {
+          ist = 0;
+          ++iu;
+        }
+      }
+      return;
+    }
+  }
   const int frow = lane & 15, g = lane >> 4;
   const int jh = ng * 16 + g * 4;                        // this lane's 4 output channels (hi rows)
   // LIN: lane-constant byte offsets of the fragment reads (output row i, k-depth d and the tap are
@@ -292,9 +326,11 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
       // first step: the next unit's source region (lands by the end of the second step); last step:
       // interpolate the next unit's patch from it into the other patch slot (published by this
       // step's barrier; the source slot is refilled only after it)
-      if (issue_p)
-        for (int j = 0; j < SPPW; ++j) dma_src(ud_next, j);
-      if (st == SPU - 1 && u + 1 < my_units) ups_interp(u + 1, ud_next);
+      if constexpr (IW == 0) {
+        if (issue_p)
+          for (int j = 0; j < SPPW; ++j) dma_src(ud_next, wave + j * 8);
+        if (st == SPU - 1 && u + 1 < my_units) ups_interp(u + 1, ud_next, tid, 512, std::integral_constant<int, UCH>{});
+      }
     } else if (issue_p) {
       for (int j = 0; j < my_pp; ++j) dma_patch(u + 1, ud_next, wave + j * 8);
     }
@@ -403,7 +439,7 @@ __global__ __launch_bounds__(512) void halo_conv_kernel(const h16* __restrict__ 
     const unsigned long long ts_pre = __builtin_amdgcn_s_memtime();
 #endif
     if constexpr (UPS) {
-      if (issue_p) dh_wait_vmcnt<SPPW>();
+      if (IW == 0 && issue_p) dh_wait_vmcnt<SPPW>();
       else dh_wait_vmcnt<0>();
     } else if (issue_p) {
       if (my_pp == PPMAX) dh_wait_vmcnt<PPMAX>();
@@ -519,7 +555,7 @@ int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias
   if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
   const int ntiles = (int)nt;
   const int grid = ntiles < cus ? ntiles : cus;
-  hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false, true>), dim3(grid), dim3(512), 0, st, (const h16*)x,
+  hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false, true, 4>), dim3(grid), dim3(768), 0, st, (const h16*)x,
                      (const h16*)w, bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu,
                      H, W, Cin, tiles_x, tiles_y, ntiles, Hs, Ws);
   VDA_LAUNCH_CHECK();
