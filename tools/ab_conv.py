@@ -1,6 +1,6 @@
 """In-process A/B of the decoder's big convs across libvda builds (tuning tool, not product code).
 
-usage: python tools/ab_conv.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes oc1,depth,rcu148]
+usage: python tools/ab_conv.py LIB_A.so[@knob=v] [LIB_B.so ...] [--rounds R] [--shapes oc1,depth,rcu148]
 oc1:    output_conv1, 3x3 256 -> 128 on the x2 bilinear resize of a [32, 148, 148, 256] map (fused)
 oc1u:   the same through the materialised resize + the plain halo conv (compare with oc1: same output)
 depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
@@ -30,7 +30,13 @@ while i < len(args):
         libs.append(args[i]); i += 1
 L = []
 for p in libs:
-    l = ctypes.CDLL(os.path.abspath(p)); _lib._declare(l); L.append(l)
+    # LIB.so@name=v: a tuning-build library with vda_debug_<name>(v) set first (a copy per setting)
+    path, _, knob = p.partition("@")
+    l = ctypes.CDLL(os.path.abspath(path)); _lib._declare(l)
+    if knob:
+        fn, _, v = knob.partition("=")
+        assert getattr(l, "vda_debug_" + fn)(int(v)) == 0
+    L.append(l)
 dev = "cuda"
 torch.manual_seed(0)
 st = torch.cuda.current_stream().cuda_stream

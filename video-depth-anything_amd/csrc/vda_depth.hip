@@ -73,9 +73,9 @@ __device__ __forceinline__ void dh_ac_coord(int o, int in, float sc, int& i0, in
 // interpolates its 16-B patch slots from LDS in fp32 (bilerp8: the resize kernel's formula and
 // op order, so the fp16 values are bit-identical) into the other patch ring slot.
 // IW (UPS only): IW extra interpolation waves (8 .. 8+IW-1) own the source staging and the
-// interpolation: they fetch unit u+1's source region at step 0 of unit u and build its patch over steps
-// 2 .. 7 (512 slots a step), beside the 8 MFMA waves' taps, which then never stop for the
-// interpolation; every wave takes every step barrier.
+// interpolation: they fetch unit u+1's source region at step 0 of unit u and build its patch over the
+// following steps (ups_interp_item, 64 IW items a step), beside the 8 MFMA waves' taps, which then never
+// stop for the interpolation; every wave takes every step barrier.
 template <int SLAB, int NROW, int TPS, bool DEPTH, bool UPS = false, int IW = 0>
 __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __restrict__ U, const h16* __restrict__ w1,
                                                         const float* __restrict__ b1, const float* __restrict__ w2,
@@ -217,6 +217,74 @@ __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __r
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the stores above are invisible to the compiler's counts
   };
+  // The interpolation waves' form of ups_interp (LIN layout): item = (patch column, channel chunk,
+  // 6-row segment).  The blend is o = fma(wy, bot, uy * top) with top / bot the horizontal blends
+  // fma(wx, B, ux * A) of source rows sy0 / sy1 at the column; a source row's horizontal blend at a
+  // column does not depend on the output row that uses it, so it is formed once per (column, source
+  // row) and carried down the segment: per pixel the ops of bilerp8_mix (bit-identical to bilerp8, the
+  // resize kernel's blend) in about half its VALU.
+  constexpr int ISEG = 3;                                // rows per item (6: 1809, 9: 1966 vs 1781 us)
+  constexpr int NITEM = (DP / ISEG) * DP * CPX;          // 432 for a 64-channel slab
+  auto ups_interp_item = [&](int u, const Ud& ud, int it) {
+    if (it >= NITEM) return;
+    const int y0 = ud.y0, x0 = ud.x0, sy_lo = ud.sy_lo, sx_lo = ud.sx_lo, SC = ud.SC;
+    const int cd = it % CPX, col = (it / CPX) % DP, seg = it / (CPX * DP);
+    const int pxg = x0 - 1 + col;
+    const bool okx = (unsigned)pxg < (unsigned)W;
+    int sx0, sx1;
+    float wx;
+    dh_ac_coord(min(max(pxg, 0), W - 1), Ws, usx, sx0, sx1, wx);
+    const float ux = 1.f - wx;
+    const int c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
+    auto hrow = [&](int sy, float (&t)[8]) {
+      const int r = (sy - sy_lo) * SC;
+      const uint4 a = *reinterpret_cast<const uint4*>(sbuf + ((r + c0) * CPX + cd) * 8);
+      const uint4 b = *reinterpret_cast<const uint4*>(sbuf + ((r + c1) * CPX + cd) * 8);
+      const unsigned A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[2 * j] = fma_mix_lo(wx, B[j], fma_mix_lo(ux, A[j], -0.f));
+        t[2 * j + 1] = fma_mix_hi(wx, B[j], fma_mix_hi(ux, A[j], -0.f));
+      }
+    };
+    float top[8], bot[8];
+    int s0 = -1, s1 = -1;
+#pragma unroll
+    for (int k = 0; k < ISEG; ++k) {
+      const int pr = seg * ISEG + k;
+      const int pyg = y0 - 1 + pr;
+      int sy0, sy1;
+      float wy;
+      dh_ac_coord(min(max(pyg, 0), H - 1), Hs, usy, sy0, sy1, wy);
+      const float uy = 1.f - wy;
+      if (sy0 != s0) {  // scale <= 1: the source rows advance by at most one per output row
+        if (sy0 == s1) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) top[e] = bot[e];
+        } else {
+          hrow(sy0, top);
+        }
+        hrow(sy1, bot);
+        s0 = sy0;
+        s1 = sy1;
+      }
+      unsigned o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float ol = fma_f32(wy, bot[2 * j], mul_f32(uy, top[2 * j]));
+        const float oh = fma_f32(wy, bot[2 * j + 1], mul_f32(uy, top[2 * j + 1]));
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        o[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{ol, oh}, h2));
+      }
+      const bool ok = okx && (unsigned)pyg < (unsigned)H;
+      const dh_u4 v = ok ? dh_u4{o[0], o[1], o[2], o[3]} : dh_u4{0u, 0u, 0u, 0u};
+      const int slot = (pr * DP + col) * PSTR + cd;
+      asm volatile("ds_write_b128 %0, %1" ::"v"((unsigned)(uintptr_t)(VDA_LDS h16*)(patch + (u & 1) * PBUF + slot * 8)),
+                   "v"(v)
+                   : "memory");
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the asm stores are invisible to the compiler's counts
+  };
   // weight pieces of step st of a unit of slab `slab` -> ring slot `wslot`
   auto dma_w = [&](int st, int slab, int wslot) {
 #pragma unroll
@@ -252,17 +320,18 @@ __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __r
     if (iwave) {
       // the interpolation waves' own step loop (same barrier sequence as the MFMA waves' loop below, no
       // accumulators live): unit u+1's source region at step 0 (waited for before step 1's barrier),
-      // its patch over steps 2 .. 7; the step barriers publish the writes (lgkmcnt(0) in ups_interp)
+      // its patch items over steps 2 .. 1 + ISTEPS (64 IW a step); the step barriers publish the writes
       constexpr int SPI = SPPW * 8 / IW;                 // source pieces per interpolation wave
-      static_assert(SPPW * 8 % IW == 0 && 6 * 128 * IW >= USL, "interpolation wave split");
+      constexpr int ISTEPS = (NITEM + 64 * IW - 1) / (64 * IW);
+      static_assert(LIN && SPPW * 8 % IW == 0 && ISTEPS <= SPU - 2, "interpolation wave split");
       int iu = 0, ist = 0;
       for (int gs = 0; gs < my_steps; ++gs) {
         if (ist == 0 && iu + 1 < my_units) {
           ud_next = make_ud(iu + 1);
           for (int j = 0; j < SPI; ++j) dma_src(ud_next, (wave - 8) + j * IW);
         }
-        if (ist >= 2 && ist < 8 && iu + 1 < my_units)
-          ups_interp(iu + 1, ud_next, (ist - 2) * 128 * IW + (tid - 512), 64 * IW, std::integral_constant<int, 2>{});
+        if (ist >= 2 && ist < 2 + ISTEPS && iu + 1 < my_units)
+          ups_interp_item(iu + 1, ud_next, (ist - 2) * 64 * IW + (tid - 512));
         if (ist == 1) dh_wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         if (++ist == SPU) {
@@ -394,22 +463,41 @@ __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __r
     }
     const bool tile_end = st == SPU - 1 && slab == units_per_tile - 1;
     if (!DEPTH && tile_end) {
-      // +bias [ReLU] -> fp16 NHWC; lane: 4 consecutive channels of pixel (row mg*4+i, col frow)
+      // +bias [ReLU] -> fp16 NHWC.  A lane holds 4 consecutive channels of pixel (row mg*4+i, col frow)
+      // per n-block; lane groups g and g^1 (lanes l, l^16) trade one n-block of each pair so that every
+      // lane stores 8 consecutive channels (16 B: half the store instructions of 8-B pieces).  Buffer
+      // stores over the frame, pixels outside the map dropped by the range check, so every lane issues
+      // exactly NB / 2 * 4 of them (the end-of-step wait below counts them).
       int bt, y0, x0;
       tile_of_unit(u, bt, y0, x0);
+      const __amdgpu_buffer_rsrc_t ys = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(yout + (long)bt * H * W * NROW), (short)0, (int)((long)H * W * NROW * 2), 0x00020000);
+      const bool godd = (g & 1) != 0;
 #pragma unroll
-      for (int a = 0; a < NB; ++a) {
-        const int n = (ng * NB + a) * 16 + g * 4;
-        const f4 bv = bias_r[DEPTH ? 0 : a];
+      for (int a = 0; a < NB; a += 2) {
+        const f4 bv0 = bias_r[DEPTH ? 0 : a], bv1 = bias_r[DEPTH ? 0 : a + 1];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int y = y0 + mg * 4 + i, x = x0 + frow;
-          f4 v = acc[a][i] + bv;
-          h4 o;
+          const f4 v0 = acc[a][i] + bv0, v1 = acc[a + 1][i] + bv1;
+          h4 o0, o1;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (h16)(relu_out ? fmaxf(v[r], 0.f) : v[r]);
-          if (y < H && x < W) *reinterpret_cast<h4*>(yout + (((long)bt * H + y) * W + x) * NROW + n) = o;
+          for (int r = 0; r < 4; ++r) {
+            o0[r] = (h16)(relu_out ? fmaxf(v0[r], 0.f) : v0[r]);
+            o1[r] = (h16)(relu_out ? fmaxf(v1[r], 0.f) : v1[r]);
+          }
+          const uint2 u0 = __builtin_bit_cast(uint2, o0), u1 = __builtin_bit_cast(uint2, o1);
+          const uint2 snd = godd ? u0 : u1;
+          float ax, bx, ay, by;
+          swap16_pair(__builtin_bit_cast(float, snd.x), ax, bx);
+          swap16_pair(__builtin_bit_cast(float, snd.y), ay, by);
+          const uint2 rcv = make_uint2(__builtin_bit_cast(unsigned, godd ? ax : bx), __builtin_bit_cast(unsigned, godd ? ay : by));
+          const u32x4 val = godd ? u32x4{rcv.x, rcv.y, u1.x, u1.y} : u32x4{u0.x, u0.y, rcv.x, rcv.y};
+          const int n = (ng * NB + a + (godd ? 1 : 0)) * 16 + (g & 2) * 4;
+          const unsigned vo = (y < H && x < W) ? (unsigned)(((y * W + x) * NROW + n) * 2) : 0x80000000u;
+          __builtin_amdgcn_raw_buffer_store_b128(val, ys, vo, 0, 0);
           acc[a][i] = f4{0.f, 0.f, 0.f, 0.f};
+          acc[a + 1][i] = f4{0.f, 0.f, 0.f, 0.f};
         }
       }
     }
@@ -440,6 +528,7 @@ __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __r
 #endif
     if constexpr (UPS) {
       if (IW == 0 && issue_p) dh_wait_vmcnt<SPPW>();
+      else if (IW > 0 && tile_end) dh_wait_vmcnt<NB / 2 * 4>();  // the next step's weights, not the tile's stores
       else dh_wait_vmcnt<0>();
     } else if (issue_p) {
       if (my_pp == PPMAX) dh_wait_vmcnt<PPMAX>();
@@ -555,6 +644,7 @@ int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias
   if (nt > 0x7fffffffL) return vda_set_error(-22, "conv: too many tiles");
   const int ntiles = (int)nt;
   const int grid = ntiles < cus ? ntiles : cus;
+  // 4 interpolation waves (1 / 2: 2571 / 2080 vs 1801 us, profiles/r05_ab_oc1_interp_waves_dconv_separable.log)
   hipLaunchKernelGGL((halo_conv_kernel<64, 128, 1, false, true, 4>), dim3(grid), dim3(768), 0, st, (const h16*)x,
                      (const h16*)w, bias, (const float*)nullptr, (const float*)nullptr, (float*)nullptr, (h16*)y, relu,
                      H, W, Cin, tiles_x, tiles_y, ntiles, Hs, Ws);
