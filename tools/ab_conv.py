@@ -6,6 +6,7 @@ oc1u:   the same through the materialised resize + the plain halo conv (compare 
 depth:  the depth tail on the [32, 296, 296, 128] output_conv1 map, resized to 518 x 518 (fused)
 rcu148: refinenet1 RCU conv, 3x3 256 -> 256 at 148^2 with pre-ReLU + ReLU
 rcu148r: the RCU's second conv (pre-ReLU, bias, + residual)
+rcu74 / l2rn: refinenet2's RCU conv1 / layer2_rn (512 -> 256) at 74^2
 l3rn / l4rn: layer3_rn / layer4_rn, 3x3 1024 -> 256 (no bias) at 37^2 / 19^2 (the strip conv; 19^2 splits)
 Outputs compared bit-for-bit against the first library's.
 """
@@ -83,6 +84,19 @@ def case(name):
             return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 148, 148, 256, 256, 3, 1, 1, 1, 0, 0,
                                 ctypes.byref(e), None, 0, st)
         return run, y, fl, [x, w, b, r, e]
+    if name in ("rcu74", "l2rn"):  # refinenet2's RCU conv1 (pre-ReLU, bias, ReLU) / layer2_rn (512 -> 256) at 74^2
+        ci = 256 if name == "rcu74" else 512
+        x = (torch.randn(32, 74, 74, ci, device=dev) * 0.5).half()
+        w = (torch.randn(256, 3, 3, ci, device=dev) * (9 * ci) ** -0.5).half()
+        b = torch.randn(256, device=dev) * 0.1
+        y = torch.empty(32, 74, 74, 256, device=dev, dtype=torch.float16)
+        e = _lib.Epilogue(rdiv=1, rmod=1, bias=b.data_ptr(), act=_lib.ACT_RELU if ci == 256 else 0)
+        fl = 2.0 * 32 * 74 * 74 * 256 * 9 * ci
+
+        def run(l):
+            return l.vda_conv2d(x.data_ptr(), w.data_ptr(), y.data_ptr(), 32, 74, 74, ci, 256, 3, 1, 1, int(ci == 256), 0,
+                                0, ctypes.byref(e), None, 0, st)
+        return run, y, fl, [x, w, b, e]
     if name == "rcu148":
         x = (torch.randn(32, 148, 148, 256, device=dev) * 0.5).half()
         w = (torch.randn(256, 3, 3, 256, device=dev) * (9 * 256) ** -0.5).half()
