@@ -3,7 +3,7 @@
 # in flight), MFMA-busy PMC per kernel class.  Outputs gpurun_out/c5_*.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-timeout -k 10 400 python3 bench.py --size 518 924 --steps 20 --warmup 4 > gpurun_out/c5_bench.log 2>&1 || exit 1
+timeout -k 10 400 python3 bench.py --size 518 924 --steps 20 --warmup 4 --cpu-baseline-frames 0 > gpurun_out/c5_bench.log 2>&1 || exit 1
 tail -1 gpurun_out/c5_bench.log | cut -c1-300
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5_stats -o run \
   -- python3 bench.py --size 518 924 --streams 1 --steps 6 --warmup 2 --cpu-baseline-frames 0 > gpurun_out/c5_rocprof_bench.log 2>&1 || exit 1
