@@ -73,7 +73,7 @@ __device__ __forceinline__ void dh_ac_coord(int o, int in, float sc, int& i0, in
 // interpolates its 16-B patch slots from LDS in fp32 (bilerp8: the resize kernel's formula and
 // op order, so the fp16 values are bit-identical) into the other patch ring slot.
 // IW (UPS only): IW extra interpolation waves (8 .. 8+IW-1) own the source staging and the
-// interpolation: they fetch unit u+1's source region at step 0 of unit u and build its patch over the
+// interpolation: they fetch unit u+1's source region at steps 0-1 of unit u and build its patch over the
 // following steps (ups_interp_item, 64 IW items a step), beside the 8 MFMA waves' taps, which then never
 // stop for the interpolation; every wave takes every step barrier.
 template <int SLAB, int NROW, int TPS, bool DEPTH, bool UPS = false, int IW = 0>
@@ -319,20 +319,23 @@ __global__ __launch_bounds__(512 + 64 * IW) void halo_conv_kernel(const h16* __r
   if constexpr (IW > 0) {
     if (iwave) {
       // the interpolation waves' own step loop (same barrier sequence as the MFMA waves' loop below, no
-      // accumulators live): unit u+1's source region at step 0 (waited for before step 1's barrier),
-      // its patch items over steps 2 .. 1 + ISTEPS (64 IW a step); the step barriers publish the writes
+      // accumulators live): unit u+1's source region in two halves at steps 0 and 1 (waited for before
+      // step 2's barrier; all at step 0 and blending from step 2: 1820 vs 1784 us), its patch items over
+      // steps 3 .. 2 + ISTEPS (64 IW a step); the step barriers publish the writes
       constexpr int SPI = SPPW * 8 / IW;                 // source pieces per interpolation wave
       constexpr int ISTEPS = (NITEM + 64 * IW - 1) / (64 * IW);
-      static_assert(LIN && SPPW * 8 % IW == 0 && ISTEPS <= SPU - 2, "interpolation wave split");
+      static_assert(LIN && SPPW * 8 % IW == 0 && ISTEPS <= SPU - 3, "interpolation wave split");
       int iu = 0, ist = 0;
       for (int gs = 0; gs < my_steps; ++gs) {
         if (ist == 0 && iu + 1 < my_units) {
           ud_next = make_ud(iu + 1);
-          for (int j = 0; j < SPI; ++j) dma_src(ud_next, (wave - 8) + j * IW);
+          for (int j = 0; j < SPI / 2; ++j) dma_src(ud_next, (wave - 8) + j * IW);
         }
-        if (ist >= 2 && ist < 2 + ISTEPS && iu + 1 < my_units)
-          ups_interp_item(iu + 1, ud_next, (ist - 2) * 64 * IW + (tid - 512));
-        if (ist == 1) dh_wait_vmcnt<0>();
+        if (ist == 1 && iu + 1 < my_units)
+          for (int j = SPI / 2; j < SPI; ++j) dma_src(ud_next, (wave - 8) + j * IW);
+        if (ist >= 3 && ist < 3 + ISTEPS && iu + 1 < my_units)
+          ups_interp_item(iu + 1, ud_next, (ist - 3) * 64 * IW + (tid - 512));
+        if (ist == 2) dh_wait_vmcnt<0>();
         __builtin_amdgcn_s_barrier();
         if (++ist == SPU) {
           ist = 0;
