@@ -104,3 +104,28 @@ def test_forward_input_checks_mirror_reference_asserts():
     # T = 1 (a single frame through the temporal blocks) is valid
     d = m(torch.randn(1, 1, 3, 28, 42, device="cuda"))
     assert d.shape == (1, 1, 28, 42) and torch.isfinite(d).all()
+
+
+@pytest.mark.parametrize("big", [200.0, 600.0])
+def test_forward_massive_residual_channels(big):
+    """The residual stream is fp16 here, fp32 in the reference's autocast forward (x + pos_embed promotes
+    to fp32 and every block's `x + ls(...)` stays fp32, block.py:104-106).  Trained DINOv2 weights carry a
+    few "massive" residual channels (hundreds) beside O(1) ones, where fp16's absolute step grows (0.125
+    at 200, 0.5 at 600).  Three channels are pushed to ~big by the patch-embed bias and every block's fc2
+    bias adds to them; the fp16 path stays within the fp16 bar of the fp32 oracle."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    sd = {k: v.clone() for k, v in recipe_state_dict("vits").items()}
+    ch = [7, 101, 250]
+    sd["pretrained.patch_embed.proj.bias"][ch] += big
+    depth = sum(1 for k in sd if k.startswith("pretrained.blocks.") and k.endswith(".mlp.fc2.bias"))
+    for i in range(depth):
+        sd[f"pretrained.blocks.{i}.mlp.fc2.bias"][ch] += big / 25
+    m = vda_amd.build_model("vits", sd, device="cuda")
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(1, 8, 3, 140, 196, generator=g)
+    d = m(x.cuda()).float().cpu()
+    ref = vda_oracle.forward(sd, "vits", x)
+    err = rel_l1(d, ref)
+    print(f"massive residual channels at ~{big:.0f}: rel-L1 vs oracle = {err:.3e}")
+    assert torch.isfinite(d).all()
+    assert err <= TOL_FP16
