@@ -1277,6 +1277,85 @@ void w8r_kernel(LabParams p, int tiles_m, int tiles_n) {
   __builtin_amdgcn_s_waitcnt(0);
 }
 
+
+// ---- overlap probe (timing only, wrong output): does the LDS-DMA staging run beside the MFMA stream when
+// waves that issue no MFMA issue it?  8 MFMA waves (2 per SIMD) run, per 32-deep K step, 12 ds_read_b128
+// fragment reads of a fixed 32-KiB LDS image + 32 v_mfma_f32_16x16x32_f16 (the product's 128 x 64 wave
+// tile), one barrier per step; the step's 32 KiB of X / W pieces (32 x 1 KiB) go into a 4-stage ring by
+//   MODE 0: nobody (MFMA only)                      MODE 1: two extra DMA waves, 16 pieces each
+//   MODE 2: the MFMA waves, 4 each (as the product) MODE 3: the DMA waves only (the MFMA waves just barrier)
+template <int MODE>
+__global__ __launch_bounds__(640) void overlap_probe_kernel(LabParams p, int tiles_m, int tiles_n, float* sink) {
+  __shared__ __attribute__((aligned(1024))) h16 smem[5 * STAGE];  // [0]: fragment image, [1..4]: the ring
+  int lane;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const bool dmaw = wave >= 8;
+  const int ntiles = tiles_m * tiles_n;
+  const int nk = p.K / BK;
+  const i4v xrs = rsrc4(p.x, (long)p.M * p.K * 2), wrs = rsrc4(p.w, (long)p.N * p.K * 2);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(VDA_LDS h16*)smem);
+  const int frow = lane & 15, fch = lane >> 4;
+  const unsigned fofs = lds0 + (unsigned)(frow * BK + ((fch ^ swz(frow)) << 3)) * 2u + (unsigned)((wave & 1) * 128 * BK * 2);
+  f4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int vb = blockIdx.x; vb < ntiles; vb += gridDim.x) {
+    int tm, tn;
+    tile_coords(vb, ntiles, tiles_m, tiles_n, tm, tn);
+    // piece q of a step: operand q >> 4 (X, W), rows 16 (q & 15) + lane / 4, 16-B chunk lane & 3
+    auto poff = [&](int q) {
+      const int r = (q & 15) * 16 + (lane >> 2), c = lane & 3;
+      const int row = (q >> 4) ? tn * 256 + r : tm * 256 + r;
+      const int lim = (q >> 4) ? p.N : p.M;
+      return row < lim ? (unsigned)(((long)row * p.K + c * 8) * 2) : 0x80000000u;
+    };
+    for (int t = 0; t < nk; ++t) {
+      const unsigned ring = lds0 + (unsigned)((1 + (t & 3)) * STAGE * 2);
+      if constexpr (MODE == 1 || MODE == 3) {
+        if (dmaw) {  // wave 8: the X pieces, wave 9: the W pieces; row block j in the scalar offset
+          const unsigned vo = poff((wave - 8) * 16);
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            dma16(wave == 8 ? xrs : wrs, vo, t * BK * 2 + j * 16 * p.K * 2, ring + (unsigned)((wave - 8) * 16 + j) * 1024u);
+          wait_vm<16>();
+        }
+      }
+      if constexpr (MODE == 2) {
+        if (!dmaw) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int q = wave * 4 + j;
+            dma16(q >> 4 ? wrs : xrs, poff(q), t * BK * 2, ring + (unsigned)q * 1024u);
+          }
+          wait_vm<4>();
+        }
+      }
+      if constexpr (MODE != 3) {
+        if (!dmaw) {
+          h8 a[8], b[4];
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[i]) : "v"(fofs), "n"(i * 16 * BK * 2));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b[i]) : "v"(fofs), "n"((256 + i * 16) * BK * 2));
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+          for (int mi = 0; mi < 8; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < 4; ++ni) mfma_m(acc[(mi * 4 + ni) & 7], a[mi], b[ni]);
+        }
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+  float sacc = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sacc += acc[i][0];
+  if (sacc == 1234.5f) sink[0] = sacc;
+}
 }  // namespace
 
 extern "C" int lab_gemm(int variant, const void* x, const void* w, void* y, const float* bias, int M, int N, int K,
@@ -1320,6 +1399,10 @@ extern "C" int lab_gemm(int variant, const void* x, const void* w, void* y, cons
     case 14: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 4>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;
     case 15: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 5>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;
     case 16: hipLaunchKernelGGL((w4b_kernel<2, 8, 4, 6>), dim3(g), dim3(256), 0, st, p, tiles_m, tiles_n); break;
+    case 70: hipLaunchKernelGGL(overlap_probe_kernel<0>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 71: hipLaunchKernelGGL(overlap_probe_kernel<1>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 72: hipLaunchKernelGGL(overlap_probe_kernel<2>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 73: hipLaunchKernelGGL(overlap_probe_kernel<3>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     default: return -22;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
