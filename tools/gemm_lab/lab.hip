@@ -1282,10 +1282,11 @@ void w8r_kernel(LabParams p, int tiles_m, int tiles_n) {
 // waves that issue no MFMA issue it?  8 MFMA waves (2 per SIMD) run, per 32-deep K step, 12 ds_read_b128
 // fragment reads of a fixed 32-KiB LDS image + 32 v_mfma_f32_16x16x32_f16 (the product's 128 x 64 wave
 // tile), one barrier per step; the step's 32 KiB of X / W pieces (32 x 1 KiB) go into a 4-stage ring by
-//   MODE 0: nobody (MFMA only)                      MODE 1: two extra DMA waves, 16 pieces each
+//   MODE 0: nobody (MFMA only)                      MODE 1: ND extra DMA waves, 32 / ND pieces each
 //   MODE 2: the MFMA waves, 4 each (as the product) MODE 3: the DMA waves only (the MFMA waves just barrier)
-template <int MODE>
-__global__ __launch_bounds__(640) void overlap_probe_kernel(LabParams p, int tiles_m, int tiles_n, float* sink) {
+//   MODE 5 / 6: as 1 / 0 with the MFMA operands in registers (no fragment reads: is the conflict the LDS?)
+template <int MODE, int ND = 2, int WD = 1>
+__global__ __launch_bounds__(512 + 64 * ND) void overlap_probe_kernel(LabParams p, int tiles_m, int tiles_n, float* sink) {
   __shared__ __attribute__((aligned(1024))) h16 smem[5 * STAGE];  // [0]: fragment image, [1..4]: the ring
   int lane;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lane));
@@ -1312,13 +1313,16 @@ __global__ __launch_bounds__(640) void overlap_probe_kernel(LabParams p, int til
     };
     for (int t = 0; t < nk; ++t) {
       const unsigned ring = lds0 + (unsigned)((1 + (t & 3)) * STAGE * 2);
-      if constexpr (MODE == 1 || MODE == 3) {
-        if (dmaw) {  // wave 8: the X pieces, wave 9: the W pieces; row block j in the scalar offset
-          const unsigned vo = poff((wave - 8) * 16);
+      if constexpr (MODE == 1 || MODE == 3 || MODE == 5) {
+        if (dmaw) {  // DMA wave d: pieces d * PPD .. (X for the first half of the waves, W for the second);
+                     // the row block in the scalar offset
+          constexpr int PPD = 32 / ND;
+          const int d = wave - 8, q0 = d * PPD;
+          const unsigned vo = poff(q0 & 16);
 #pragma unroll
-          for (int j = 0; j < 16; ++j)
-            dma16(wave == 8 ? xrs : wrs, vo, t * BK * 2 + j * 16 * p.K * 2, ring + (unsigned)((wave - 8) * 16 + j) * 1024u);
-          wait_vm<16>();
+          for (int j = 0; j < PPD; ++j)
+            dma16((q0 >> 4) ? wrs : xrs, vo, t * BK * 2 + ((q0 & 15) + j) * 16 * p.K * 2, ring + (unsigned)(q0 + j) * 1024u);
+          wait_vm<PPD * WD>();  // WD steps of pieces left in flight
         }
       }
       if constexpr (MODE == 2) {
@@ -1334,6 +1338,16 @@ __global__ __launch_bounds__(640) void overlap_probe_kernel(LabParams p, int til
       if constexpr (MODE != 3) {
         if (!dmaw) {
           h8 a[8], b[4];
+          if constexpr (MODE >= 5) {  // operands from registers: no LDS traffic in the MFMA waves
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] = h8{(h16)(lane & 7), 0, 0, 0, 0, 0, 0, (h16)i};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b[i] = h8{(h16)(lane & 3), 0, 0, 0, 0, 0, 0, (h16)i};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(a[i]));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(b[i]));
+          } else {
 #pragma unroll
           for (int i = 0; i < 8; ++i)
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(a[i]) : "v"(fofs), "n"(i * 16 * BK * 2));
@@ -1341,6 +1355,7 @@ __global__ __launch_bounds__(640) void overlap_probe_kernel(LabParams p, int til
           for (int i = 0; i < 4; ++i)
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(b[i]) : "v"(fofs), "n"((256 + i * 16) * BK * 2));
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
 #pragma unroll
           for (int mi = 0; mi < 8; ++mi)
 #pragma unroll
@@ -1403,6 +1418,16 @@ extern "C" int lab_gemm(int variant, const void* x, const void* w, void* y, cons
     case 71: hipLaunchKernelGGL(overlap_probe_kernel<1>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     case 72: hipLaunchKernelGGL(overlap_probe_kernel<2>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     case 73: hipLaunchKernelGGL(overlap_probe_kernel<3>, dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 80: hipLaunchKernelGGL((overlap_probe_kernel<3, 4, 2>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 81: hipLaunchKernelGGL((overlap_probe_kernel<3, 4, 3>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 82: hipLaunchKernelGGL((overlap_probe_kernel<5, 4, 3>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 83: hipLaunchKernelGGL((overlap_probe_kernel<1, 4, 3>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 78: hipLaunchKernelGGL((overlap_probe_kernel<5, 2>), dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 79: hipLaunchKernelGGL((overlap_probe_kernel<6, 2>), dim3(g), dim3(640), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 74: hipLaunchKernelGGL((overlap_probe_kernel<1, 4>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 75: hipLaunchKernelGGL((overlap_probe_kernel<3, 4>), dim3(g), dim3(768), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 76: hipLaunchKernelGGL((overlap_probe_kernel<1, 8>), dim3(g), dim3(1024), 0, st, p, tiles_m, tiles_n, (float*)y); break;
+    case 77: hipLaunchKernelGGL((overlap_probe_kernel<3, 8>), dim3(g), dim3(1024), 0, st, p, tiles_m, tiles_n, (float*)y); break;
     default: return -22;
   }
   return hipGetLastError() == hipSuccess ? 0 : -1;
