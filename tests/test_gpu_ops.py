@@ -136,6 +136,27 @@ def test_conv3x3(cin, cout, stride, H, W, BT):
     assert rel(y, ref.permute(0, 2, 3, 1)) < 2e-3
 
 
+@pytest.mark.parametrize("cin,cout,H,W,BT", [(1024, 1024, 37, 37, 12), (512, 256, 60, 60, 8), (256, 512, 31, 45, 16)])
+def test_conv3x3_stride2_im2col_route(cin, cout, H, W, BT):
+    """Stride-2 3x3 convs with >= 4096 output pixels (the DPT reassemble's resize_layers[3], dpt.py:77-82)
+    run as an explicit im2col into the workspace + the dense GEMM: bit-identical to the implicit-GEMM
+    conv (the same K order), and vs torch fp32."""
+    x = rnd(BT, cin, H, W, seed=21)
+    w = rnd(cout, cin, 3, 3, scale=(9 * cin) ** -0.5, seed=22)
+    b = rnd(cout, scale=0.1, seed=23)
+    xh, wh = h(x.permute(0, 2, 3, 1)), h(w.permute(0, 2, 3, 1))
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    assert vda_amd._libvda().vda_conv2d_workspace(BT, H, W, cin, cout, 3, 2, 1) == BT * Ho * Wo * 9 * cin * 2
+    y = ops.conv2d(xh, wh, stride=2, bias=f32(b))
+    T = tune_lib()
+    with T.route(force_tile=-2):  # every special route off: the implicit-GEMM conv
+        assert T.lib.vda_conv2d_workspace(BT, H, W, cin, cout, 3, 2, 1) == 0
+        y_imp = T.conv2d(xh, wh, stride=2, bias=f32(b))
+    assert torch.equal(y, y_imp)
+    ref = F.conv2d(x, w, b, stride=2, padding=1).permute(0, 2, 3, 1)
+    assert rel(y, ref) < 2e-3
+
+
 def test_conv3x3_rcu_fusion_epilogue():
     """out = x0 + conv2(relu(conv1(relu(x1)))) + x1  (blocks.py:78-91, :146-150)."""
     BT, C, H, W = 2, 64, 10, 13

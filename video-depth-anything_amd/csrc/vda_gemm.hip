@@ -60,6 +60,8 @@ int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const f
 int vda_row_partials_launch(const void* y, int64_t ldy, float* out, int32_t rows, int32_t N, hipStream_t st);
 // halo-tiled phased 3x3 conv, Cout = 256 (vda_hconv.hip)
 bool vda_conv_hconv_serves(int BT, int H, int W, int Cin, int Cout);
+int vda_conv_im2col(const void* x, void* a, int BT, int H, int W, int Cin, int Ho, int Wo, int ks, int stride, int pad,
+                    hipStream_t st);
 int vda_conv_hconv(const void* x, const void* w, void* y, const float* bias, int relu_out, int pre_relu,
                    const void* res, const void* res2, int res2_h, int res2_w, int BT, int H, int W, int Cin, int Cout,
                    hipStream_t st);
@@ -2046,6 +2048,21 @@ static bool conv_takes_strip(int BT, int H, int W, int Cin, int Cout, int ks, in
   return g_force_tile == -3 || (g_force_tile == -1 && (Cin >= 512 || strip_tiles * 2 <= cu_count()));
 }
 
+// Stride-2 3x3 convs (the DPT reassemble's resize_layers[3], dpt.py:77-82: 1024 -> 1024 at 37^2 -> 19^2):
+// explicit im2col into the workspace + the dense phased GEMM.  The implicit-GEMM conv runs its K steps at
+// about half the dense rate, and at 184 tiles x 144 K steps (32 frames) the copy costs far less than that
+// (410 -> 210 us of GEMM for ~70 us of copy, tools/archive/s2conv_probe.py); bit-identical (same K order).
+static long conv_im2col_bytes(int BT, int H, int W, int Cin, int ks, int stride, int pad) {
+  const long Ho = (H + 2L * pad - ks) / stride + 1, Wo = (W + 2L * pad - ks) / stride + 1;
+  return (long)BT * Ho * Wo * ks * ks * Cin * 2;
+}
+static bool conv_takes_im2col(int BT, int H, int W, int Cin, int Cout, int ks, int stride, int pad, int up_h) {
+  if (up_h > 0 || ks != 3 || stride != 2 || Cin % 64 != 0 || Cout % 256 != 0 || g_force_tile != -1) return false;
+  const long Ho = (H + 2L * pad - ks) / stride + 1, Wo = (W + 2L * pad - ks) / stride + 1;
+  const long M = (long)BT * Ho * Wo;
+  return Ho > 0 && Wo > 0 && M >= 4096 && conv_im2col_bytes(BT, H, W, Cin, ks, stride, pad) < (1L << 31);
+}
+
 // the halo-tiled 256-channel conv route (the only one whose epilogue reads an upsampled res2)
 static bool conv_takes_hconv(int BT, int H, int W, int Cin, int Cout, int ks, int stride, int pad) {
   return ks == 3 && stride == 1 && pad == 1 && g_force_tile == -1 && vda_conv_hconv_serves(BT, H, W, Cin, Cout);
@@ -2055,6 +2072,7 @@ extern "C" int64_t vda_conv2d_workspace(int32_t BT, int32_t H, int32_t W, int32_
                                         int32_t stride, int32_t pad) {
   if (BT <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0) return 0;
   if (conv_takes_hconv(BT, H, W, Cin, Cout, ks, stride, pad)) return 0;
+  if (conv_takes_im2col(BT, H, W, Cin, Cout, ks, stride, pad, 0)) return conv_im2col_bytes(BT, H, W, Cin, ks, stride, pad);
   if (!conv_takes_strip(BT, H, W, Cin, Cout, ks, stride, pad, 0)) return 0;
   return vda_conv_strip_ws_bytes(BT, H, W, Cin, Cout);
 }
@@ -2133,6 +2151,14 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
       !p.epi.gamma && !p.epi.rowbias && (long)H * W >= 128L * 128L) {
     rc = vda_conv_halo(x, w, y, p.epi.bias, p.epi.act == VDA_ACT_RELU, BT, H, W, Cin, Cout, (hipStream_t)stream);
     if (rc != 1) return rc;
+  }
+  if (conv_takes_im2col(BT, H, W, Cin, Cout, ks, stride, pad, 0) && !pre_relu && ws &&
+      ws_bytes >= conv_im2col_bytes(BT, H, W, Cin, ks, stride, pad) && (uintptr_t)ws % 16 == 0) {
+    rc = vda_conv_im2col(x, ws, BT, H, W, Cin, p.Ho, p.Wo, ks, stride, pad, (hipStream_t)stream);
+    if (rc) return rc;
+    p.x = (const h16*)ws;
+    p.ldx = p.K;
+    return launch<false>(p, (hipStream_t)stream);
   }
   return launch<true>(p, (hipStream_t)stream);
 }

@@ -121,7 +121,39 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ i
   }
 }
 
+// Explicit im2col of an NHWC fp16 map for a ks x ks conv: A[m = (bt, oy, ox)][k = (ky, kx, ci)] — the
+// K order of the [Cout, ks, ks, Cin] weights, so the dense GEMM on A sums the same products in the same
+// order as the implicit-GEMM conv (bit-identical).  One 16-B chunk per thread; block y = output pixel.
+__global__ __launch_bounds__(256) void conv_im2col_kernel(const h16* __restrict__ x, h16* __restrict__ a, int M, int H,
+                                                          int W, int Cin, int Ho, int Wo, int ks, int stride, int pad) {
+  const int cpt = Cin >> 3;                          // 16-B chunks per tap
+  const int cpr = ks * ks * cpt;                     // per row of A
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cpr) return;
+  const int tap = c / cpt, cc = c - tap * cpt;
+  const int ky = tap / ks, kx = tap - ky * ks;
+  for (int m = blockIdx.y; m < M; m += gridDim.y) {
+    const int hw = Ho * Wo;
+    const int bt = m / hw, r = m - bt * hw, oy = r / Wo, ox = r - oy * Wo;
+    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if ((unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W)
+      v = ldg16(x + (((long)bt * H + iy) * W + ix) * Cin + cc * 8);
+    stg16(a + (long)m * cpr * 8 + c * 8, v);
+  }
+}
+
 }  // namespace
+
+// A [BT*Ho*Wo, ks*ks*Cin] for the explicit-im2col conv route (vda_gemm.hip); Cin % 8 == 0
+int vda_conv_im2col(const void* x, void* a, int BT, int H, int W, int Cin, int Ho, int Wo, int ks, int stride, int pad,
+                    hipStream_t st) {
+  const int M = BT * Ho * Wo, cpr = ks * ks * (Cin / 8);
+  hipLaunchKernelGGL(conv_im2col_kernel, dim3((unsigned)((cpr + 255) / 256), (unsigned)std::min(M, 65535)), dim3(256), 0,
+                     st, (const h16*)x, (h16*)a, M, H, W, Cin, Ho, Wo, ks, stride, pad);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t H, int32_t W, int32_t C,
                                      int32_t Ho, int32_t Wo, void* stream) {
