@@ -180,14 +180,16 @@ def test_torch_ops_registered_meta_shapes_and_no_cpu_kernel():
 
 def test_workspace_queries():
     """Workspaces are the caller's (no library-global device buffers): the strip conv's split
-    workspace is sized by vda_conv2d_workspace, the depth head's resize workspace by
+    workspace and the stride-2 conv's im2col matrix are sized by vda_conv2d_workspace, the depth head's resize workspace by
     vda_depth_head_workspace (0 when the fused kernel serves the shape)."""
     lib = _lib.lib()
     # ViT-L layer4_rn at 19^2 (32 frames, Cin 1024 -> 256): split into fp32 slices of M x 256
     n = lib.vda_conv2d_workspace(32, 19, 19, 1024, 256, 3, 1, 1)
     assert n > 0 and n % (32 * 19 * 19 * 256 * 4) == 0
     assert lib.vda_conv2d_workspace(32, 148, 148, 256, 256, 3, 1, 1) == 0   # implicit GEMM: no workspace
-    assert lib.vda_conv2d_workspace(32, 37, 37, 1024, 256, 3, 2, 1) == 0    # stride 2: no workspace
+    # stride 2 with >= 4096 output pixels: the explicit im2col matrix [32*19*19, 9*1024] fp16
+    assert lib.vda_conv2d_workspace(32, 37, 37, 1024, 256, 3, 2, 1) == 32 * 19 * 19 * 9 * 1024 * 2
+    assert lib.vda_conv2d_workspace(4, 37, 37, 1024, 256, 3, 2, 1) == 0     # small M: the implicit GEMM
     assert lib.vda_depth_head_workspace(32, 296, 296, 128, 518, 518) == 0   # fused resize: none
     assert lib.vda_depth_head_workspace(2, 20, 20, 32, 518, 518) == 0   # C % 32: fused depth conv
     assert lib.vda_depth_head_workspace(2, 20, 20, 40, 518, 518) == 2 * 518 * 518 * 40 * 2  # C % 32 != 0: materialised
