@@ -2153,7 +2153,8 @@ extern "C" int vda_conv2d(const void* x, const void* w, void* y, int32_t BT, int
     if (rc != 1) return rc;
   }
   if (conv_takes_im2col(BT, H, W, Cin, Cout, ks, stride, pad, 0) && !pre_relu && ws &&
-      ws_bytes >= conv_im2col_bytes(BT, H, W, Cin, ks, stride, pad) && (uintptr_t)ws % 16 == 0) {
+      ws_bytes >= conv_im2col_bytes(BT, H, W, Cin, ks, stride, pad) && (uintptr_t)ws % 16 == 0 &&
+      (uintptr_t)x % 16 == 0) {
     rc = vda_conv_im2col(x, ws, BT, H, W, Cin, p.Ho, p.Wo, ks, stride, pad, (hipStream_t)stream);
     if (rc) return rc;
     p.x = (const h16*)ws;
