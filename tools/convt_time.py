@@ -21,3 +21,19 @@ for k, c in ((4, 256), (2, 512)):
     us = s.elapsed_time(e) * 1000 / n
     flop = 2.0 * BT * h * w * k * k * c * c
     print(f"ConvT k{k}s{k} {c}ch BT={BT} {h}x{w}: {us:.1f} us  {flop / us / 1e6:.0f} TF/s")
+    # the same GEMM with a plain row store (no pixel shuffle) and torch's copy rate for the output bytes
+    y = torch.empty(BT * h * w, k * k * c, device="cuda", dtype=torch.float16)
+    s.record()
+    for _ in range(n):
+        ops.gemm(x, wp, bias=b, out=y)
+    e.record()
+    e.synchronize()
+    ug = s.elapsed_time(e) * 1000 / n
+    z = torch.empty_like(y)
+    s.record()
+    for _ in range(n):
+        z.copy_(y)
+    e.record()
+    e.synchronize()
+    uc = s.elapsed_time(e) * 1000 / n
+    print(f"   row-store GEMM {ug:.1f} us; output {y.numel() * 2 / 1e6:.0f} MB, a device copy of it {uc:.1f} us")
