@@ -11,7 +11,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 nfw = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 # forwards are delimited by the patch-embed im2col dispatch
-starts = [i for i, r in enumerate(rows) if "im2col" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "im2col" in r["Kernel_Name"] and "conv_im2col" not in r["Kernel_Name"]]
 s0 = starts[-1]
 s1 = len(rows)
 tot = defaultdict(float)
