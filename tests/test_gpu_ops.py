@@ -927,7 +927,7 @@ def test_gemm_dynamic_tile_schedule(M, N, K, kind):
     assert ops.sched_counters().dtype == torch.int32 and ops.sched_counters() is ops.sched_counters()
 
 
-@pytest.mark.parametrize("BT,H,W", [(2, 70, 518), (3, 28, 924), (1, 14, 1036)])
+@pytest.mark.parametrize("BT,H,W", [(2, 70, 518), (3, 28, 924), (1, 14, 1036), (1, 518, 518), (32, 518, 518)])
 def test_patch_im2col_exact(BT, H, W):
     """patch_embed.py:69-82 input: the [BT, 1 + np, Kp] fp16 patch matrix is the exact fp16 of the
     image's 14 x 14 patches (channel-major: k = c * 196 + ky * 14 + kx), zero cls rows and zero K padding."""

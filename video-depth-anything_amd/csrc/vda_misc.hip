@@ -90,34 +90,53 @@ __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x
 }
 
 // A[BT*(1+np), Kp]: row 0 of each frame (cls) is zero; k = ci*196 + ky*14 + kx; zero pad k >= 588.
+// Block = (up to gp patches of one patch row, patch row py, frame bt): the 3 x 14 image rows under
+// those patches are read once, coalesced (8 B per lane: W and the group start are even), rounded to
+// fp16 into LDS, then the group's A rows — contiguous in A — are written as 16-B chunks gathered
+// from LDS.  The rounding is the same (h16)float as element-wise, so A is bit-identical.
 __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ img, h16* __restrict__ a, int BT, int H,
-                                                     int W, int Kp) {
-  const int ph = H / 14, pw = W / 14, np = ph * pw;
-  const int kc = Kp >> 3;
-  const long total = (long)BT * (1 + np) * kc;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
-    const int c8 = (int)(i % kc);
-    const long row = i / kc;
-    const int tok = (int)(row % (1 + np));
-    const int bt = (int)(row / (1 + np));
-    h8 o;
-    if (tok == 0) {
+                                                     int W, int Kp, int gp) {
+  extern __shared__ h16 s[];  // [ci * 14 + ky][x - x0], 42 x gp * 14
+  const int pw = W / 14, np = (H / 14) * pw;
+  const int py = blockIdx.y, bt = blockIdx.z, p0 = blockIdx.x * gp;
+  const int ng = min(gp, pw - p0);  // patches in this block
+  const int x0 = p0 * 14, srow = gp * 14;
+  const int r2 = ng * 7;            // float2 per staged row
+  const float* src = img + (long)bt * 3 * H * W + (long)(py * 14) * W + x0;
+  constexpr int U = 8;  // loads in flight per thread (42 x 91 float2 = 15 per thread at gp = 13)
+  for (int t0 = threadIdx.x; t0 < 42 * r2; t0 += 256 * U) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    f2v v[U];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = (h16)0;
-    } else {
-      const int p = tok - 1, py = p / pw, px = p - py * pw;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = c8 * 8 + j;
-        float v = 0.f;
-        if (k < 588) {
-          const int ci = k / 196, r = k - ci * 196, ky = r / 14, kx = r - ky * 14;
-          v = img[(((long)bt * 3 + ci) * H + py * 14 + ky) * W + px * 14 + kx];
-        }
-        o[j] = (h16)v;
-      }
+    for (int j = 0; j < U; ++j) {
+      const int t = t0 + j * 256, row = t / r2, c2 = t - row * r2;
+      const int ci = row / 14, ky = row - ci * 14;
+      if (t < 42 * r2) v[j] = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(src + ((long)ci * H + ky) * W + 2 * c2));
     }
-    stg16(a + i * 8, __builtin_bit_cast(uint4, o));
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const int t = t0 + j * 256, row = t / r2, c2 = t - row * r2;
+      typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+      if (t < 42 * r2) *reinterpret_cast<h2v*>(&s[row * srow + 2 * c2]) = h2v{(h16)v[j].x, (h16)v[j].y};
+    }
+  }
+  __syncthreads();
+  const int kc = Kp >> 3;
+  h16* const arow = a + ((long)bt * (1 + np) + 1 + (long)py * pw + p0) * Kp;
+  for (int q = threadIdx.x; q < ng * kc; q += 256) {
+    const int pl = q / kc, c8 = q - pl * kc;
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = c8 * 8 + j;
+      const int ci = k / 196, r = k - ci * 196, ky = r / 14, kx = r - ky * 14;
+      o[j] = k < 588 ? s[(ci * 14 + ky) * srow + pl * 14 + kx] : (h16)0;
+    }
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(arow + (long)q * 8));
+  }
+  if (py == 0 && blockIdx.x == 0) {  // the frame's cls row
+    h16* const crow = a + (long)bt * (1 + np) * Kp;
+    for (int c8 = threadIdx.x; c8 < kc; c8 += 256) stg16(crow + c8 * 8, make_uint4(0u, 0u, 0u, 0u));
   }
 }
 
@@ -177,9 +196,15 @@ extern "C" int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H
   VDA_CHECK_ARG(BT > 0 && H >= 14 && W >= 14, "empty image");
   VDA_CHECK_ARG(H % 14 == 0 && W % 14 == 0, "input height/width must be multiples of the patch size 14");
   VDA_CHECK_ARG(Kp >= 588 && Kp % 8 == 0, "Kp must be >= 588 and a multiple of 8");
-  const long total = (long)BT * (1 + (H / 14) * (W / 14)) * (Kp / 8);
-  const int grid = (int)std::min<long>((total + 255) / 256, 65536);
-  hipLaunchKernelGGL(im2col_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, img, (h16*)a, BT, H, W, Kp);
+  VDA_CHECK_ARG(H / 14 <= 65535 && BT <= 65535, "image too tall or batch too large");
+  const int pw = W / 14;
+  // 13 patches per block, fewer while that leaves < 2,048 blocks (tools/ab_im2col.py over 37 .. 3:
+  // 41-44 us at 32 x 518^2, 13-19 best; 3 at 2 x 70 x 518, where 13 takes 8 us)
+  int gp = std::min(pw, 13);
+  auto nblk = [&](int g) { return (long)BT * (H / 14) * ((pw + g - 1) / g); };
+  while (gp > 3 && nblk(gp) < 2048) gp = std::max(3, (gp + 1) / 2);
+  const dim3 grid((unsigned)((pw + gp - 1) / gp), (unsigned)(H / 14), (unsigned)BT);
+  hipLaunchKernelGGL(im2col_kernel, grid, dim3(256), 42 * gp * 14 * 2, (hipStream_t)stream, img, (h16*)a, BT, H, W, Kp, gp);
   VDA_LAUNCH_CHECK();
   return 0;
 }
