@@ -1,6 +1,6 @@
 """In-process A/B of the encoder GEMMs across libvda builds (tuning tool, not product code).
 
-usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so ...] [--rounds R] [--shapes qkv,proj,fc1,fc2] [--m M]
+usage: python tools/ab_gemm.py LIB_A.so [LIB_B.so[@tile=N] ...] [--rounds R] [--shapes qkv,proj,fc1,fc2,patch] [--m M]
 
 Each library is loaded through ctypes and called through the C ABI (vda_gemm) on the current torch
 stream with the forward's exact epilogues (LN fold from [M, 4, 2] partials for qkv / fc1, residual +
@@ -33,8 +33,17 @@ while i < len(args):
 L = []
 for k, p in enumerate(libs):
     path, _, opt = p.partition("@")
+    if opt:  # LIB@tile=N: a private copy of a tuning build with vda_debug_force_tile(N)
+        import shutil, tempfile
+        cp = os.path.join(tempfile.mkdtemp(), "libvda.so")
+        shutil.copy(path, cp)
+        path = cp
     l = ctypes.CDLL(os.path.abspath(path))
     _lib._declare(l)
+    if opt:
+        key, _, val = opt.partition("=")
+        assert key == "tile", opt
+        l.vda_debug_force_tile(int(val))
     L.append(l)
 
 dev = "cuda"
@@ -50,6 +59,15 @@ def row_partials(y):  # [M, N] fp16 -> [M, ceil(N/256), 2] (sum, sumsq) fp32, as
 
 
 def mk(name):
+    if name == "patch":  # the patch embed: K 588 -> 640, per-token fp32 row bias (pos embed + bias)
+        K, N, ntok = 640, C, 1370
+        x = (torch.randn(M, K, device=dev)).half()
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).half()
+        rb = torch.randn(ntok, N, device=dev)
+        e = _lib.Epilogue()
+        e.rowbias = rb.data_ptr(); e.rdiv = 1; e.rmod = ntok
+        y = torch.empty(M, N, device=dev, dtype=torch.float16)
+        return dict(x=x, w=w, y=y, e=e, K=K, N=N, keep=[x, w, rb], res=None, ldy=N)
     if name == "ff1":  # a motion module's GEGLU feed-forward (the [h | g] interleaved W, N/2 outputs)
         K, N = C, 8 * C
         x = tok

@@ -1431,8 +1431,9 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
       if (e.rowbias) {  // per-row bias (folded positional terms): 4 loads per output row group
         // (m / rdiv) % rmod by fp32 reciprocals + one integer correction each (m < 2^24: exact)
         const float inv_div = 1.f / (float)e.rdiv, inv_mod = 1.f / (float)e.rmod;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
+        // RBD row groups in flight: the row-bias table (the patch embed's 5.6 MB) is not L2-resident,
+        // so one group at a time pays 8 MALL round trips per tile
+        auto rb_load = [&](int j, f4 (&rb)[4]) {
           const int m = m0 + wm * 128 + j * 16 + mcol;
           int qd = (int)((float)m * inv_div);
           qd += (m - qd * e.rdiv >= e.rdiv) ? 1 : 0;
@@ -1441,12 +1442,19 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
           qm += (qd - qm * e.rmod >= e.rmod) ? 1 : 0;
           qm -= (qd < qm * e.rmod) ? 1 : 0;
           const long roff = m < p.M ? (long)(qd - qm * e.rmod) * p.N : 0;
-          f4 rb[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) rb[i] = *reinterpret_cast<const f4*>(e.rowbias + roff + ncl[i]);
+        };
+        constexpr int RBD = 2;  // tools/ab_gemm.py --shapes patch: 1: 97.2, 2: 91.8, 3: 97.5 us
+        f4 rb[RBD][4];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[i][j] += rb[i];
-          __builtin_amdgcn_sched_barrier(0);  // keep the loads of row group j+1 after these adds
+        for (int j = 0; j < RBD - 1; ++j) rb_load(j, rb[j]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (j + RBD - 1 < 8) rb_load(j + RBD - 1, rb[(j + RBD - 1) % RBD]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i][j] += rb[j % RBD][i];
+          __builtin_amdgcn_sched_barrier(0);  // keep the loads of row group j+RBD after these adds
         }
       }
     }
