@@ -284,6 +284,7 @@ __global__ __launch_bounds__(64) void gn_finalize_kernel(const h16* __restrict__
   const int lane = threadIdx.x;
   float a1 = 0.f, a2 = 0.f;
   const int n = nchunk * cg;
+#pragma unroll 8  // loads in flight; the sums keep their order
   for (int i = lane; i < n; i += 64) {
     const int chn = i / cg, c = g * cg + (i - chn * cg);
     const float* p = part + ((long)(f * nchunk + chn) * C + c) * 2;
