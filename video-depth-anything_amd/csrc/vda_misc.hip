@@ -43,27 +43,38 @@ __device__ __forceinline__ void ac_coord(int o, int in, int out, int& i0, int& i
   w = ac_weight(sc, (float)o, i0);
 }
 
-// One block row per output row (bt, oy): the two source rows and the y weight are fixed per block,
-// and the (ox, 8-channel chunk) index within a row needs only 32-bit math.  (The first version
-// decomposed a flat 64-bit index per element: the 64-bit div/mod sequence held it at ~2.5 TB/s.)
-// Each thread writes UP x 16 B of the row, loads issued before any math.
+// One block row per PAIR of output rows (bt, oy), (bt, oy + 1): the two source rows and the y weight
+// are fixed per row, and the (ox, 8-channel chunk) index within a row needs only 32-bit math.  When
+// both rows blend the same two source rows (every upscale by >= 2 pairs them), the second row reuses
+// the first's four corner loads: half the L2 reads per output.  (The first version decomposed a flat
+// 64-bit index per element: the 64-bit div/mod sequence held it at ~2.5 TB/s.)  Each thread writes
+// UP x 16 B of each row, loads issued before any math.
 template <int UP>
 __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x, h16* __restrict__ y, int rows,
                                                        int H, int W, int C, int Ho, int Wo) {
   const unsigned nch = (unsigned)C >> 3;
   const unsigned row_items = (unsigned)Wo * nch;
   const float sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
-  for (int r = blockIdx.y; r < rows; r += gridDim.y) {
+  for (int r = 2 * blockIdx.y; r < rows; r += 2 * gridDim.y) {
     const int bt = r / Ho, oy = r - bt * Ho;
     int y0, y1; float wy;
     ac_coord(oy, H, Ho, y0, y1, wy);
+    const bool two = r + 1 < rows;
+    const int btB = (r + 1) / Ho, oyB = r + 1 - btB * Ho;
+    int y0B, y1B; float wyB;
+    ac_coord(oyB, H, Ho, y0B, y1B, wyB);
+    const bool share = btB == bt && y0B == y0 && y1B == y1;
     const h16* r0 = x + ((long)bt * H + y0) * W * C;
     const h16* r1 = x + ((long)bt * H + y1) * W * C;
+    const h16* r0B = x + ((long)btB * H + y0B) * W * C;
+    const h16* r1B = x + ((long)btB * H + y1B) * W * C;
     h16* out = y + (long)r * row_items * 8;
+    h16* outB = out + (long)row_items * 8;
     const unsigned step = gridDim.x * 256u;
     for (unsigned i0 = blockIdx.x * 256u * UP + threadIdx.x; i0 < row_items; i0 += step * UP) {
       h8 a[UP], b[UP], c[UP], d[UP];
       float wx[UP];
+      unsigned o0[UP], o1[UP];
 #pragma unroll
       for (int u = 0; u < UP; ++u) {
         const unsigned i = min(i0 + u * 256u, row_items - 1);
@@ -71,11 +82,12 @@ __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x
         const float f = sx * (float)ox;
         const int x0 = (int)f, x1 = min(x0 + 1, W - 1);
         wx[u] = f - (float)x0;
-        const unsigned o0 = (unsigned)x0 * C + ch * 8, o1 = (unsigned)x1 * C + ch * 8;
-        a[u] = __builtin_bit_cast(h8, ldg16(r0 + o0));
-        b[u] = __builtin_bit_cast(h8, ldg16(r0 + o1));
-        c[u] = __builtin_bit_cast(h8, ldg16(r1 + o0));
-        d[u] = __builtin_bit_cast(h8, ldg16(r1 + o1));
+        o0[u] = (unsigned)x0 * C + ch * 8;
+        o1[u] = (unsigned)x1 * C + ch * 8;
+        a[u] = __builtin_bit_cast(h8, ldg16(r0 + o0[u]));
+        b[u] = __builtin_bit_cast(h8, ldg16(r0 + o1[u]));
+        c[u] = __builtin_bit_cast(h8, ldg16(r1 + o0[u]));
+        d[u] = __builtin_bit_cast(h8, ldg16(r1 + o1[u]));
       }
 #pragma unroll
       for (int u = 0; u < UP; ++u) {
@@ -83,6 +95,24 @@ __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x
         if (i < row_items) {
           const h8 o = bilerp8(a[u], b[u], c[u], d[u], wx[u], wy);
           __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(out + (long)i * 8));
+        }
+      }
+      if (!two) continue;
+      if (!share) {
+#pragma unroll
+        for (int u = 0; u < UP; ++u) {
+          a[u] = __builtin_bit_cast(h8, ldg16(r0B + o0[u]));
+          b[u] = __builtin_bit_cast(h8, ldg16(r0B + o1[u]));
+          c[u] = __builtin_bit_cast(h8, ldg16(r1B + o0[u]));
+          d[u] = __builtin_bit_cast(h8, ldg16(r1B + o1[u]));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < UP; ++u) {
+        const unsigned i = i0 + u * 256u;
+        if (i < row_items) {
+          const h8 o = bilerp8(a[u], b[u], c[u], d[u], wx[u], wyB);
+          __builtin_nontemporal_store(__builtin_bit_cast(u32x4, o), reinterpret_cast<u32x4*>(outB + (long)i * 8));
         }
       }
     }
@@ -183,7 +213,7 @@ extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t
   VDA_CHECK_ARG(row_items < (1L << 30) && (long)W * C < (1L << 31), "resize row too wide");
   const int gx = (int)((row_items + 256 * UP - 1) / (256 * UP));
   const int rows = BT * Ho;
-  const int gy = std::min(rows, 65535);
+  const int gy = std::min((rows + 1) / 2, 65535);
   hipLaunchKernelGGL(upsample_kernel<UP>, dim3(gx, gy), dim3(256), 0, (hipStream_t)stream, (const h16*)x, (h16*)y,
                      rows, H, W, C, Ho, Wo);
   VDA_LAUNCH_CHECK();
