@@ -199,6 +199,10 @@ def main():
     pending = []  # async gathers in flight (two steps deep)
     gbufs = ([[None] * world for _ in range(2)]) if gather else None
 
+    if not args.dry_run:
+        # the packed weights and the token bias are built lazily by the first forward; build them here,
+        # on the current stream, before any side stream can read them (the video driver does the same)
+        model.prepare(dev, (H, W))
     strs = []
     if args.streams > 1 and dev.type == "cuda":
         strs = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]

@@ -209,6 +209,7 @@ int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t H, int32_t
  * them) -> A [BT*(1+np), Kp] half with np = (H/14)*(W/14), K order (ci, ky, kx), zero-padded to
  * Kp >= 588, and an all-zero row 0 per frame for the cls token.  Followed by vda_gemm with a
  * per-token rowbias this replaces patch_embed.py:69-82 + dinov2.py:212-219 (cls cat, pos add).
+ * img must be 8-byte aligned and a 16-byte aligned (vector loads / stores); -22 otherwise.
  */
 int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W, int32_t Kp,
                      void* stream);

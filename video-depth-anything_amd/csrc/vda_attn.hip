@@ -4,6 +4,18 @@
 #include <type_traits>
 #include <stdlib.h>
 
+#ifdef VDA_TS  // per-block clock stamps of the spatial attention (tools/clock_probe.py; experiments only)
+__device__ unsigned long long g_atsc[8192][4];
+#define ATSC(k) do { if (threadIdx.x == 0 && blockIdx.x < 8192) { \
+    g_atsc[blockIdx.x][2 * (k)] = __builtin_amdgcn_s_memtime(); \
+    g_atsc[blockIdx.x][2 * (k) + 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+extern "C" int vda_debug_attn_clock_stamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_atsc), sizeof(g_atsc), 0, hipMemcpyDeviceToHost);
+}
+#else
+#define ATSC(k) do {} while (0)
+#endif
+
 namespace {
 
 // =============================================================================================
@@ -228,14 +240,30 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 // behind set A or in plain order: 317.8 / 307.8 vs 275.0 us, bit-identical (r05_ab_attn_two_sets.log).
 // =============================================================================================
 constexpr int SA_KT = 64;    // keys per tile
-constexpr int SA_QB = 128;   // queries per block
-constexpr int SA_NBUF = 3;   // K/V ring depth
+// block shape (A/B builds override): waves per block, K/V ring depth, min waves per SIMD (VGPR budget)
+#ifndef SA_NW
+#define SA_NW 4
+#endif
+#ifndef SA_NBUF
+#define SA_NBUF 3
+#endif
+#ifndef SA_WPE
+#define SA_WPE 2
+#endif
+#ifndef SA_HALF
+#define SA_HALF 0
+#endif
 
 __device__ __forceinline__ int sa_kslot(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 __device__ __forceinline__ int sa_vslot(int row, int c) { return row * 8 + (c ^ (((row >> 1) & 1) << 2)); }
-__global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                                int N, int H, int nqb, int nblocks, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) h16 sKV[SA_NBUF][2][SA_KT * SD];
+template <int NW, int NBUF, int WPE, bool HALF>
+__global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                                      int N, int H, int nqb, int nblocks, float scale_log2) {
+  constexpr int QB = 32 * NW;    // queries per block
+  constexpr int PPW = 16 / NW;   // K/V DMA pieces per wave per tile
+  static_assert(NBUF >= 2 && NBUF <= 4 && (NW == 4 || NW == 8), "ring depth 2..4, 4 or 8 waves");
+  __shared__ __attribute__((aligned(16))) h16 sKV[NBUF][2][SA_KT * SD];
+  ATSC(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int id = blockIdx.x;
@@ -247,7 +275,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
   const long ld = 3L * C;
   const h16* base = qkv + (long)b * N * ld + h * SD;
   const int r32 = lane & 31, hf = lane >> 5;
-  const int q = qb * SA_QB + wave * 32 + r32;
+  const int q = qb * QB + wave * 32 + r32;
 
   h8 qf[4];
 #pragma unroll
@@ -263,19 +291,19 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
   // with the (b, h) rows as the record range: keys >= N read as zeros.  Per-lane offsets are fixed
   // across tiles (the tile advances by the scalar offset).
   const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
-  unsigned voff[4];
+  unsigned voff[PPW];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
+  for (int j = 0; j < PPW; ++j) {
+    const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
     const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
     const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
     voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
   }
   auto dma = [&](int kt) {
-    const int buf = kt % SA_NBUF;
+    const int buf = kt % NBUF;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
+    for (int j = 0; j < PPW; ++j) {
+      const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
                                                (int)(kt * SA_KT * ld * 2), 0, 0);
     }
@@ -309,9 +337,83 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
     // ring slot byte offset through an opaque scalar move: the compiler would otherwise strength-reduce
     // kt % 3 into per-read address updates (two VALU per read)
     unsigned bo;
-    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % SA_NBUF), "n"(2 * SA_KT * SD * 2));
+    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % NBUF), "n"(2 * SA_KT * SD * 2));
     const char* kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
     const char* vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
+    if constexpr (HALF) {
+      // the softmax unit is a 32-key half of the tile (key block kb): its 4 QK MFMAs, 16 exponentials
+      // and 4 PV MFMAs, with half the score / P registers live
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        f16x s1;
+        auto qk1 = [&]() {
+#pragma unroll
+          for (int ks = 0; ks < 4; ++ks) {
+            const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
+            s1 = mfma32(kf, qf[ks], ks == 0 ? negm : s1);
+          }
+          if constexpr (MASK) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) s1[r] = -INFINITY;
+          }
+        };
+        auto max1 = [&]() {
+          float mx = fmaxf(fmaxf(s1[0], s1[1]), s1[2]);
+#pragma unroll
+          for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s1[r]), s1[r + 1]);
+          mx = fmaxf(mx, s1[15]);
+          return half_max(mx);
+        };
+        auto rebase1 = [&](float sh) {
+          mrun += sh;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) negm[r] = -mrun;
+          s1 -= sh;
+        };
+        h8 p2[2];
+        float tt;
+        auto expo1 = [&]() {
+          tt = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(s1[r]);
+            tt += pv;
+            p2[r >> 3][r & 7] = (h16)pv;
+          }
+        };
+        qk1();
+        if (FIRST && kb == 0) {
+          rebase1(max1());
+          expo1();
+        } else {
+          expo1();
+          if (__any(!(tt <= 32768.f))) {  // rare: re-base this half on its true max and redo it
+            qk1();
+            const float sh = fmaxf(max1(), 0.f);
+            const float alpha = __builtin_amdgcn_exp2f(-sh);
+            lsum *= alpha;
+            o[0] *= alpha;
+            o[1] *= alpha;
+            rebase1(sh);
+            expo1();
+          }
+        }
+        lsum += tt;
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const char* va = vbase + vofs[dt] + (kb * 2 + ps) * 2048;
+            const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
+            const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
+            const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+            o[dt] = mfma32(vf, p2[ps], o[dt]);
+          }
+        }
+      }
+      return;
+    }
     f16x sc[2];
     auto qk = [&]() {
 #pragma unroll
@@ -393,14 +495,20 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
     }
   };
   const int ntiles = (N + SA_KT - 1) / SA_KT;
-  auto enter = [&](int kt) {  // tile kt landed and visible; ring slot of kt-1 free -> prefetch kt+2
-    if (kt + 1 < ntiles) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  auto enter = [&](int kt) {  // tile kt landed and visible; ring slot of kt-1 free -> prefetch kt+NBUF-1
+    // this wave's DMA issued after tile kt's: tiles kt+1 .. min(kt+NBUF-2, ntiles-1), PPW pieces each
+    const int later = min(NBUF - 2, ntiles - 1 - kt);
+    if (later <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (later * PPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (later * PPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (later * PPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (kt + 2 < ntiles) dma(kt + 2);
+    if (kt + NBUF - 1 < ntiles) dma(kt + NBUF - 1);
   };
-  dma(0);
-  if (ntiles > 1) dma(1);
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (i < ntiles) dma(i);
   const bool tail = N % SA_KT != 0;
   enter(0);
   if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{});
@@ -428,6 +536,7 @@ __global__ __launch_bounds__(256, 2) void spatial_attn32_kernel(const h16* __res
         *reinterpret_cast<h4*>(op + dt * 32 + 8 * gq + 4 * hf) = v;
       }
   }
+  ATSC(1);
 }
 
 // =============================================================================================
@@ -701,11 +810,11 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
     hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, scale * 1.4426950408889634f);
   } else {
-    const int nqb = (N + SA_QB - 1) / SA_QB;
+    const int nqb = (N + 32 * SA_NW - 1) / (32 * SA_NW);
     const long nb = (long)nqb * H * B;
     VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
-    hipLaunchKernelGGL(spatial_attn32_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
-                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
+    hipLaunchKernelGGL((spatial_attn32_kernel<SA_NW, SA_NBUF, SA_WPE, (bool)SA_HALF>), dim3((unsigned)nb), dim3(64 * SA_NW), 0,
+                       (hipStream_t)stream, (const h16*)qkv, (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
   }
   VDA_LAUNCH_CHECK();
   return 0;

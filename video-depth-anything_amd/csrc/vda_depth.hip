@@ -639,6 +639,7 @@ int vda_depth_halo_fused(const void* x, const void* w1, const float* b1, const f
 int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int Hs, int Ws,
                         int H, int W, int Cin, int Cout, hipStream_t st) {
   if (Cout != 128 || Cin % 64 != 0 || Hs > H || Ws > W || Hs < 1 || Ws < 1) return 1;
+  if ((long)H * W * Cout * 2 >= (1L << 31)) return 1;  // the epilogue's per-frame buffer stores take 32-bit offsets
   const float sy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f, sx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
   if (((int)(17.f * sy) + 3) * ((int)(17.f * sx) + 3) > 192) return 1;
   const int cus = vda_cu_count();
@@ -661,6 +662,7 @@ int vda_conv_halo_fused(const void* x, const void* w, void* y, const float* bias
 int vda_conv_halo(const void* x, const void* w, void* y, const float* bias, int relu, int BT, int H, int W, int Cin,
                   int Cout, hipStream_t st) {
   if (Cout != 128 || Cin % 64 != 0) return 1;
+  if ((long)H * W * Cout * 2 >= (1L << 31)) return 1;  // the epilogue's per-frame buffer stores take 32-bit offsets
   const int cus = vda_cu_count();
   const int tiles_x = (W + DT - 1) / DT, tiles_y = (H + DT - 1) / DT;
   const long nt = (long)BT * tiles_x * tiles_y;

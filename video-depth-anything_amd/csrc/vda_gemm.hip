@@ -24,8 +24,18 @@ __device__ unsigned long long g_ts[4096][8];
 extern "C" int vda_debug_timestamps(void* host) {
   return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ts), sizeof(g_ts), 0, hipMemcpyDeviceToHost);
 }
+// per-block clock stamps of the persistent GEMM (tools/clock_probe.py): s_memtime (shader clock) and
+// s_memrealtime (100 MHz) at block start and end, so clock = d(memtime) / d(realtime) x 100 MHz
+__device__ unsigned long long g_tsc[1024][4];
+#define TSC(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) { \
+    g_tsc[blockIdx.x][2 * (k)] = __builtin_amdgcn_s_memtime(); \
+    g_tsc[blockIdx.x][2 * (k) + 1] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+extern "C" int vda_debug_clock_stamps(void* host) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_tsc), sizeof(g_tsc), 0, hipMemcpyDeviceToHost);
+}
 #else
 #define TS(k) do {} while (0)
+#define TSC(k) do {} while (0)
 #endif
 #include "../../include/vda.h"
 
@@ -747,8 +757,11 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
   // ConvTranspose(k = s) pixel-shuffle stores through the staged row epilogue when a 256-wide N tile is
   // 256 consecutive channels of ONE output pixel (cout % 256 == 0): its rows are then whole 512-B output
   // pixel runs at remapped addresses (phase 2 below), instead of 8-byte scatter stores per element
-  const bool ps_rows = !EK && ACT != VDA_ACT_GEGLU && !ROWB && XR == 2 && p.epi.store == VDA_STORE_PIXEL_SHUFFLE &&
-                       p.epi.ps_cout % 256 == 0 && p.epi.ps_win >= 16 && (long)p.M * p.N * 2 < 0x7fffffffL;
+  // (WR == 2: a 256-wide N tile, 16 rows per store iteration, the only shape ps_store is compiled for; the
+  // 16-B row-run stores need a 16-B aligned y)
+  const bool ps_rows = !EK && ACT != VDA_ACT_GEGLU && !ROWB && XR == 2 && WR == 2 &&
+                       p.epi.store == VDA_STORE_PIXEL_SHUFFLE && p.epi.ps_cout % 256 == 0 && p.epi.ps_win >= 16 &&
+                       (long)p.M * p.N * 2 < 0x7fffffffL && (uintptr_t)p.y % 16 == 0;
   const bool rows_store = EK ? true : (p.epi.store == VDA_STORE_ROWS || ps_rows);
   const bool has_res = EK == 2 ? true : (EK == 1 || EK == 3) ? false : p.epi.res != nullptr;
   const bool has_res2 = EK ? false : p.epi.res2 != nullptr;
@@ -1789,6 +1802,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
     const int tbase = (int)gridDim.x + (int)(blockIdx.x & 7);
     int* tslot = XR == 2 ? reinterpret_cast<int*>(smem + SMEM_HALVES - 64) : nullptr;
     bool pre = false;
+    TSC(0);
     for (int vb = blockIdx.x; vb >= 0 && vb < ntiles;) {
       TS(0);
       const int nxt = vb + (int)gridDim.x;
@@ -1798,6 +1812,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
       pre = chain;
       TS(7);
     }
+    TSC(1);
     if (dyn && wave == 0 && threadIdx.x == 0) {
       // the block has drawn its last ticket (retired by its tile's waits): the last block to leave zeroes
       // the counters for the next launch on this stream

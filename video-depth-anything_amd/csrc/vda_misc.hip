@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void upsample_kernel(const h16* __restrict__ x
         const unsigned ox = i / nch, ch = i - ox * nch;
         const float f = sx * (float)ox;
         const int x0 = (int)f, x1 = min(x0 + 1, W - 1);
-        wx[u] = f - (float)x0;
+        wx[u] = ac_weight(sx, (float)ox, x0);  // one explicit fma, as at every fused-resize site
         o0[u] = (unsigned)x0 * C + ch * 8;
         o1[u] = (unsigned)x1 * C + ch * 8;
         a[u] = __builtin_bit_cast(h8, ldg16(r0 + o0[u]));
@@ -223,6 +223,8 @@ extern "C" int vda_upsample_bilinear(const void* x, void* y, int32_t BT, int32_t
 extern "C" int vda_patch_im2col(const float* img, void* a, int32_t BT, int32_t H, int32_t W, int32_t Kp,
                                 void* stream) {
   VDA_CHECK_ARG(img && a, "null pointer");
+  // the LDS-staged kernel reads img in 8-byte vectors and writes A in 16-byte chunks
+  VDA_CHECK_ARG((uintptr_t)img % 8 == 0 && (uintptr_t)a % 16 == 0, "img must be 8-byte and a 16-byte aligned");
   VDA_CHECK_ARG(BT > 0 && H >= 14 && W >= 14, "empty image");
   VDA_CHECK_ARG(H % 14 == 0 && W % 14 == 0, "input height/width must be multiples of the patch size 14");
   VDA_CHECK_ARG(Kp >= 588 && Kp % 8 == 0, "Kp must be >= 588 and a multiple of 8");
