@@ -245,14 +245,32 @@ constexpr int SA_KT = 64;    // keys per tile
 #define SA_NW 4
 #endif
 #ifndef SA_NBUF
-#define SA_NBUF 3
+#define SA_NBUF 2
 #endif
 #ifndef SA_WPE
-#define SA_WPE 2
+#define SA_WPE 4
 #endif
 #ifndef SA_HALF
-#define SA_HALF 0
+#define SA_HALF 1
 #endif
+#ifndef SA_STATIC  // 2-deep ring as two __shared__ objects, tile loop unrolled by 2 (see the kernel)
+#define SA_STATIC 1
+#endif
+#ifndef SA_KPRE  // half path: the 4 K fragment reads issued before the QK chain (A/B)
+#define SA_KPRE 0
+#endif
+#ifndef SA_PRIO  // s_setprio 1 around the half path's MFMA clusters (A/B)
+#define SA_PRIO 1
+#endif
+#ifndef SA_DOT2  // row sums of the fp16-rounded P by v_dot2_f32_f16 against (1, 1): half the adds
+#define SA_DOT2 0
+#endif
+__device__ __forceinline__ float sa_psum(const h8& p, float acc) {
+  const h2 one = h2{(h16)1.f, (h16)1.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_fdot2(h2{p[2 * i], p[2 * i + 1]}, one, acc, false);
+  return acc;
+}
 
 __device__ __forceinline__ int sa_kslot(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 __device__ __forceinline__ int sa_vslot(int row, int c) { return row * 8 + (c ^ (((row >> 1) & 1) << 2)); }
@@ -262,7 +280,12 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
   constexpr int QB = 32 * NW;    // queries per block
   constexpr int PPW = 16 / NW;   // K/V DMA pieces per wave per tile
   static_assert(NBUF >= 2 && NBUF <= 4 && (NW == 4 || NW == 8), "ring depth 2..4, 4 or 8 waves");
-  __shared__ __attribute__((aligned(16))) h16 sKV[NBUF][2][SA_KT * SD];
+  // STAT (2-deep ring): the two slots are distinct __shared__ objects and the tile loop is unrolled by
+  // 2, so a tile's LDS reads and the DMA in flight into the other slot are provably disjoint (with one
+  // ring array hipcc drains that DMA, s_waitcnt vmcnt(0), in front of every tile's first V read)
+  constexpr bool STAT = NBUF == 2 && SA_STATIC;
+  __shared__ __attribute__((aligned(16))) h16 sKV[STAT ? 1 : NBUF][2][SA_KT * SD];
+  __shared__ __attribute__((aligned(16))) h16 sKV1[STAT ? 2 : 1][STAT ? SA_KT * SD : 8];
   ATSC(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -304,8 +327,19 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
 #pragma unroll
     for (int j = 0; j < PPW; ++j) {
       const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)&sKV[buf][isv][pc * 512], 16, (int)voff[j],
-                                               (int)(kt * SA_KT * ld * 2), 0, 0);
+      h16* dst = &sKV[STAT ? 0 : buf][isv][pc * 512];
+      if (STAT && buf == 1) dst = &sKV1[isv][pc * 512];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)dst, 16, (int)voff[j], (int)(kt * SA_KT * ld * 2), 0, 0);
+    }
+  };
+  // STAT: the same with the slot a compile-time constant (the unrolled loop's DMA)
+  auto dma_s = [&](int kt, auto slot_tag) {
+    constexpr int SL = decltype(slot_tag)::value;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
+      h16* dst = SL == 0 ? &sKV[0][isv][pc * 512] : &sKV1[isv][pc * 512];
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)dst, 16, (int)voff[j], (int)(kt * SA_KT * ld * 2), 0, 0);
     }
   };
 
@@ -331,15 +365,26 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
   // fit fp16: the scores are recomputed, the true tile max taken and the tile redone), so the steady
   // state computes no max at all.  P <= 2^15 keeps P exact to fp16 rounding and the fp32 sums far
   // from overflow.
-  auto tile = [&](int kt, auto first_tag, auto mask_tag) {
+  auto tile = [&](int kt, auto first_tag, auto mask_tag, auto slot_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MASK = decltype(mask_tag)::value;
+    constexpr int SL = decltype(slot_tag)::value;  // STAT: the tile's slot (-1: from kt)
     // ring slot byte offset through an opaque scalar move: the compiler would otherwise strength-reduce
     // kt % 3 into per-read address updates (two VALU per read)
-    unsigned bo;
-    asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % NBUF), "n"(2 * SA_KT * SD * 2));
-    const char* kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
-    const char* vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
+    const char* kbase;
+    const char* vbase;
+    if constexpr (SL >= 0) {
+      kbase = reinterpret_cast<const char*>(SL == 0 ? sKV[0][0] : sKV1[0]);
+      vbase = reinterpret_cast<const char*>(SL == 0 ? sKV[0][1] : sKV1[1]);
+    } else if constexpr (STAT) {
+      kbase = reinterpret_cast<const char*>((kt & 1) ? sKV1[0] : sKV[0][0]);
+      vbase = reinterpret_cast<const char*>((kt & 1) ? sKV1[1] : sKV[0][1]);
+    } else {
+      unsigned bo;
+      asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % NBUF), "n"(2 * SA_KT * SD * 2));
+      kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
+      vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
+    }
     if constexpr (HALF) {
       // the softmax unit is a 32-key half of the tile (key block kb): its 4 QK MFMAs, 16 exponentials
       // and 4 PV MFMAs, with half the score / P registers live
@@ -347,10 +392,19 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
       for (int kb = 0; kb < 2; ++kb) {
         f16x s1;
         auto qk1 = [&]() {
+          if (SA_KPRE) {  // the half's 4 K fragments requested together, then the MFMA chain
+            h8 kf[4];
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) s1 = mfma32(kf[ks], qf[ks], ks == 0 ? negm : s1);
+          } else {
 #pragma unroll
           for (int ks = 0; ks < 4; ++ks) {
             const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
             s1 = mfma32(kf, qf[ks], ks == 0 ? negm : s1);
+          }
           }
           if constexpr (MASK) {
 #pragma unroll
@@ -374,15 +428,17 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
         h8 p2[2];
         float tt;
         auto expo1 = [&]() {
-          tt = 0.f;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float pv = __builtin_amdgcn_exp2f(s1[r]);
-            tt += pv;
+            if (!SA_DOT2) tt = r == 0 ? pv : tt + pv;  // (no add of 0 to start the chain)
             p2[r >> 3][r & 7] = (h16)pv;
           }
+          if (SA_DOT2) tt = sa_psum(p2[1], sa_psum(p2[0], 0.f));
         };
+        if (SA_PRIO) __builtin_amdgcn_s_setprio(1);
         qk1();
+        if (SA_PRIO) __builtin_amdgcn_s_setprio(0);
         if (FIRST && kb == 0) {
           rebase1(max1());
           expo1();
@@ -400,6 +456,7 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
           }
         }
         lsum += tt;
+        if (SA_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
 #pragma unroll
@@ -411,6 +468,7 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
             o[dt] = mfma32(vf, p2[ps], o[dt]);
           }
         }
+        if (SA_PRIO) __builtin_amdgcn_s_setprio(0);
       }
       return;
     }
@@ -460,10 +518,16 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
-          if (kb == 0) t0 += pv;
-          else t1 += pv;
+          if (!SA_DOT2) {
+            if (kb == 0) t0 += pv;
+            else t1 += pv;
+          }
           pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
         }
+      if (SA_DOT2) {
+        t0 = sa_psum(pf[1], sa_psum(pf[0], 0.f));
+        t1 = sa_psum(pf[3], sa_psum(pf[2], 0.f));
+      }
     };
     if constexpr (FIRST) {
       rebase(tile_max());
@@ -510,17 +574,36 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
   for (int i = 0; i < NBUF - 1; ++i)
     if (i < ntiles) dma(i);
   const bool tail = N % SA_KT != 0;
+  using dyn_slot = std::integral_constant<int, -1>;
   enter(0);
-  if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{});
-  else tile(0, std::true_type{}, std::false_type{});
+  if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{}, dyn_slot{});
+  else tile(0, std::true_type{}, std::false_type{}, dyn_slot{});
   const int nfull = ntiles - (tail ? 1 : 0);
-  for (int kt = 1; kt < nfull; ++kt) {
+  int kt = 1;
+  if constexpr (STAT) {
+    // pairs (odd kt in slot 1, even kt + 1 in slot 0); enter() of each issues the next tile's DMA into
+    // the slot the previous tile read
+    using s0 = std::integral_constant<int, 0>;
+    using s1 = std::integral_constant<int, 1>;
+    auto enter_s = [&](int k, auto next_slot) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k landed (NBUF 2: no newer pieces in flight)
+      __builtin_amdgcn_s_barrier();
+      if (k + 1 < ntiles) dma_s(k + 1, next_slot);
+    };
+    for (; kt + 1 < nfull; kt += 2) {
+      enter_s(kt, s0{});
+      tile(kt, std::false_type{}, std::false_type{}, s1{});
+      enter_s(kt + 1, s1{});
+      tile(kt + 1, std::false_type{}, std::false_type{}, s0{});
+    }
+  }
+  for (; kt < nfull; ++kt) {
     enter(kt);
-    tile(kt, std::false_type{}, std::false_type{});
+    tile(kt, std::false_type{}, std::false_type{}, dyn_slot{});
   }
   if (tail && ntiles > 1) {
     enter(ntiles - 1);
-    tile(ntiles - 1, std::false_type{}, std::true_type{});
+    tile(ntiles - 1, std::false_type{}, std::true_type{}, dyn_slot{});
   }
   // epilogue: lane holds Oᵀ[d = dt*32 + 8gq + 4hf + r][q]
   const float inv = 1.f / half_sum(lsum);
