@@ -589,6 +589,38 @@ def test_gemm_layernorm_fold(M, N, K, act):
     assert err < max(2 * err0, 2e-3)
 
 
+@pytest.mark.parametrize("M,C", [(43808, 1024), (21904, 256), (4001, 256), (361, 1024), (300, 384)])
+def test_gemm_layernorm_fold_geglu(M, C):
+    """The motion modules' ff_norm folded into the GEGLU GEMM (motion_module.py:182, attention.py:363-384):
+    the producer of the residual stream (to_out + residual) writes the row statistics (stats_out), the
+    GEGLU GEMM applies rstd (h W'^T - mean colsum) + W beta + b to both halves before the gate, vs torch
+    fp32 LayerNorm -> Linear -> GEGLU on the same stored fp16 residual.  Large M takes the phased
+    256x256 kernel (LN-fold staged epilogue), small M the tile kernels (epi_geglu4)."""
+    g = torch.Generator().manual_seed(M + C)
+    inner = 4 * C
+    a = (torch.randn(M, C, generator=g) * 0.5).half().float()          # attention output
+    hres = (torch.randn(M, C, generator=g) * 2 + 1).half().float()    # residual stream before to_out
+    wo, bo = torch.randn(C, C, generator=g) * C ** -0.5, 0.1 * torch.randn(C, generator=g)
+    gam, bet = 1 + 0.2 * torch.randn(C, generator=g), 0.1 * torch.randn(C, generator=g)
+    w1, b1 = torch.randn(2 * inner, C, generator=g) * C ** -0.5, 0.1 * torch.randn(2 * inner, generator=g)
+    st = torch.empty(M + 1, (C + 255) // 256, 2, device=DEV)
+    hd = ops.gemm(h(a), h(wo), bias=f32(bo), res=h(hres), stats_out=st)  # to_out + residual, row statistics
+    hv = hd.float().cpu()
+    wg = _geglu_interleave(w1 * gam[None, :]).half()
+    y = ops.gemm(hd, wg.to(DEV), bias=f32(_geglu_interleave(w1 @ bet + b1)), act=ACT_GEGLU, ln_stats=st,
+                 ln_parts=st.shape[1], ln_eps=1e-5, ln_colsum=f32(wg.float().sum(1)))
+    hh, gg = F.linear(F.layer_norm(hv, (C,), gam, bet, eps=1e-5), w1, b1).chunk(2, -1)
+    ref = hh * F.gelu(gg)
+    err = rel(y, ref)
+    # the unfused fp16 path for scale: LayerNorm output rounded to fp16, then the GEGLU GEMM
+    y0 = ops.gemm(ops.layernorm(hd, f32(gam), f32(bet), 1e-5), h(_geglu_interleave(w1)), bias=f32(_geglu_interleave(b1)),
+                  act=ACT_GEGLU)
+    err0 = rel(y0, ref)
+    print(f"LN-folded GEGLU GEMM {M}x{2 * inner}x{C}: rel-L1 {err:.2e} (unfused fp16 path {err0:.2e})")
+    assert y.shape == (M, inner)
+    assert err < max(2 * err0, 2e-3)
+
+
 @pytest.mark.parametrize("C,S,T,B", [(256, 300, 8, 2), (1024, 361, 4, 3), (256, 1369, 5, 1), (256, 256, 16, 1)])
 def test_gemm_layernorm_fold_rowbias(C, S, T, B):
     """Motion-module q/k/v with its LayerNorm folded (motion_module.py:175, the EK 3 register epilogue):

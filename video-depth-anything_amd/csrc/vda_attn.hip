@@ -217,75 +217,44 @@ __global__ __launch_bounds__(256) void spatial_attn_kernel(const h16* __restrict
 }
 
 // =============================================================================================
-// Spatial attention v2, D = 64, v_mfma_f32_32x32x16_f16 (the 32-cycle MFMA leaves 24 issue cycles
-// per gap for the softmax VALU, the 16x16x32 one only 8).  Block = 4 waves x 32 queries of one
-// (batch, head); a wave owns 32 query columns, a lane q = lane & 31 and half hf = lane >> 5.
+// Spatial attention, D = 64, v_mfma_f32_32x32x16_f16 (the 32-cycle MFMA leaves 24 issue cycles per
+// gap for the softmax VALU, the 16x16x32 one only 8).  Block = 4 waves x 32 queries of one (batch,
+// head); a wave owns 32 query columns, a lane q = lane & 31 and half hf = lane >> 5.
 //   Sᵀ[key][q] = K·Qᵀ   A = K rows (LDS, ds_read_b128), B = Q (registers, pre-scaled by scale·log2e);
 //                       the chain starts from C = -m (a 16-register tile of the running reference
 //                       m, see the deferred re-base below), so the scores come out relative to it
 //                       with no VALU subtraction.
 //   Oᵀ += Vᵀ·Pᵀ         B = P straight from the Sᵀ registers (k order 16st + 8(j>>2) + 4hf + (j&3)),
 //                       A = Vᵀ by ds_read_b64_tr_b16 in the same permuted key order.
-// K/V tiles (64 keys x 64 channels, 8 KiB each) arrive by LDS-DMA into a 3-deep ring (4 x 1-KiB
-// pieces per wave per tile, keys >= N from a zero page), one barrier per tile.  The block -> (b, h,
-// query block) map keeps all query blocks of one (b, h) on one XCD (K/V re-reads hit that L2).
-// LDS images: K slot row*8 + (chunk ^ ((row >> 1) & 7)), V slot row*8 + (chunk ^ (((row >> 1) & 1) << 2)):
-// conflict-free for the b128 K reads and the b64 transposed V reads (brute-forced).
-// 152 VGPRs: three blocks per CU (3 x 48 KiB of LDS).  Measured and rejected (tools/ab_attn.py):
-// issuing the QK MFMAs of tile t+1 before the softmax of tile t (213 VGPRs, a 4-slot ring, two blocks
-// per CU) 333 vs 292 us; with the per-tile max still computed, 354 vs 320 us; each 32-key half of a
-// tile exponentiated, checked and multiplied into O on its own (so half 0's softmax can sit beside
-// half 1's QK MFMAs): 302 vs 297 us.  Round 5: two 32-query sets per wave (every K / Vᵀ fragment read
-// feeds two MFMAs; 251 VGPRs, two blocks of 4 x 64 queries per CU, 4-deep ring), with set B half a tile
-// behind set A or in plain order: 317.8 / 307.8 vs 275.0 us, bit-identical (r05_ab_attn_two_sets.log).
+// K/V tiles (64 keys x 64 channels, 8 KiB each) arrive by LDS-DMA (4 x 1-KiB pieces per wave per
+// tile, keys >= N read as zeros) into a 2-slot ring, one barrier per tile.  The softmax unit is a
+// 32-key half of the tile: its 4 QK MFMAs, 16 exponentials and 4 PV MFMAs, so only half a tile of
+// scores / P is live: 119 VGPRs, FOUR waves per SIMD (4 blocks x 32 KiB of LDS per CU), which cover
+// each other's LDS / MFMA / exp latency chains better than three waves of whole-tile work (152 VGPRs).
+// The two ring slots are two __shared__ objects and the tile loop is unrolled by 2 with static slots:
+// with one ring array hipcc cannot prove that a tile's V reads do not alias the DMA in flight into the
+// other slot and drains it (s_waitcnt vmcnt(0)) before every tile's first V read.  s_setprio 1 around
+// the MFMA clusters lets a wave that reaches its MFMAs issue them ahead of the other waves' softmax VALU.
+// The block -> (b, h, query block) map keeps all query blocks of one (b, h) on one XCD (K/V re-reads
+// hit that L2).  LDS images: K slot row*8 + (chunk ^ ((row >> 1) & 7)), V slot row*8 + (chunk ^
+// (((row >> 1) & 1) << 2)): conflict-free for the b128 K reads and the b64 transposed V reads.
+// Measured (tools/ab_attn.py, same box, ViT-L 32 x 1370 x 16): whole-tile softmax, 3-slot ring, three
+// waves per SIMD (round 5) 292-298 us; halves at three waves per SIMD 297; halves + 4 waves/SIMD 282-289;
+// + static slots 276; + s_setprio 272-275 (r06_ab_attn_*.log).  Rejected: 8-wave blocks (297-302),
+// row sums by v_dot2 on the packed P (+3 %), the half's K reads issued ahead of the chain (no change),
+// and a software-pipelined wave (the next half's QK chain issued under the current half's softmax,
+// 3-slot ring, 2 / 3 waves per SIMD: 343 / 330 us, bit-identical: profiles/r06_ab_attn_pipe.log).
+// Earlier rounds: QK of tile t+1 before the softmax of tile t 333 vs 292 us; two 32-query sets per
+// wave 317.8 / 307.8 vs 275.0 us (r05_ab_attn_two_sets.log).
 // =============================================================================================
 constexpr int SA_KT = 64;    // keys per tile
-// block shape (A/B builds override): waves per block, K/V ring depth, min waves per SIMD (VGPR budget)
-#ifndef SA_NW
-#define SA_NW 4
-#endif
-#ifndef SA_NBUF
-#define SA_NBUF 2
-#endif
-#ifndef SA_WPE
-#define SA_WPE 4
-#endif
-#ifndef SA_HALF
-#define SA_HALF 1
-#endif
-#ifndef SA_STATIC  // 2-deep ring as two __shared__ objects, tile loop unrolled by 2 (see the kernel)
-#define SA_STATIC 1
-#endif
-#ifndef SA_KPRE  // half path: the 4 K fragment reads issued before the QK chain (A/B)
-#define SA_KPRE 0
-#endif
-#ifndef SA_PRIO  // s_setprio 1 around the half path's MFMA clusters (A/B)
-#define SA_PRIO 1
-#endif
-#ifndef SA_DOT2  // row sums of the fp16-rounded P by v_dot2_f32_f16 against (1, 1): half the adds
-#define SA_DOT2 0
-#endif
-__device__ __forceinline__ float sa_psum(const h8& p, float acc) {
-  const h2 one = h2{(h16)1.f, (h16)1.f};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_fdot2(h2{p[2 * i], p[2 * i + 1]}, one, acc, false);
-  return acc;
-}
 
 __device__ __forceinline__ int sa_kslot(int row, int c) { return row * 8 + (c ^ ((row >> 1) & 7)); }
 __device__ __forceinline__ int sa_vslot(int row, int c) { return row * 8 + (c ^ (((row >> 1) & 1) << 2)); }
-template <int NW, int NBUF, int WPE, bool HALF>
-__global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
-                                                                      int N, int H, int nqb, int nblocks, float scale_log2) {
-  constexpr int QB = 32 * NW;    // queries per block
-  constexpr int PPW = 16 / NW;   // K/V DMA pieces per wave per tile
-  static_assert(NBUF >= 2 && NBUF <= 4 && (NW == 4 || NW == 8), "ring depth 2..4, 4 or 8 waves");
-  // STAT (2-deep ring): the two slots are distinct __shared__ objects and the tile loop is unrolled by
-  // 2, so a tile's LDS reads and the DMA in flight into the other slot are provably disjoint (with one
-  // ring array hipcc drains that DMA, s_waitcnt vmcnt(0), in front of every tile's first V read)
-  constexpr bool STAT = NBUF == 2 && SA_STATIC;
-  __shared__ __attribute__((aligned(16))) h16 sKV[STAT ? 1 : NBUF][2][SA_KT * SD];
-  __shared__ __attribute__((aligned(16))) h16 sKV1[STAT ? 2 : 1][STAT ? SA_KT * SD : 8];
+__global__ __launch_bounds__(256, 4) void spatial_attn32_kernel(const h16* __restrict__ qkv, h16* __restrict__ out,
+                                                                int N, int H, int nqb, int nblocks, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) h16 sKV0[2][SA_KT * SD];  // ring slot 0: [K | V]
+  __shared__ __attribute__((aligned(16))) h16 sKV1[2][SA_KT * SD];  // ring slot 1
   ATSC(0);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -298,7 +267,7 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
   const long ld = 3L * C;
   const h16* base = qkv + (long)b * N * ld + h * SD;
   const int r32 = lane & 31, hf = lane >> 5;
-  const int q = qb * QB + wave * 32 + r32;
+  const int q = qb * 128 + wave * 32 + r32;
 
   h8 qf[4];
 #pragma unroll
@@ -314,32 +283,27 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
   // with the (b, h) rows as the record range: keys >= N read as zeros.  Per-lane offsets are fixed
   // across tiles (the tile advances by the scalar offset).
   const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)((long)N * ld * 2), 0x00020000);
-  unsigned voff[PPW];
+  unsigned voff[4];
 #pragma unroll
-  for (int j = 0; j < PPW; ++j) {
-    const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
+  for (int j = 0; j < 4; ++j) {
+    const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
     const int slot = pc * 64 + lane, row = slot >> 3, pos = slot & 7;
     const int c = isv ? (pos ^ (((row >> 1) & 1) << 2)) : (pos ^ ((row >> 1) & 7));
     voff[j] = (unsigned)(((long)row * ld + (isv ? 2 * C : C) + c * 8) * 2);
   }
-  auto dma = [&](int kt) {
-    const int buf = kt % NBUF;
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
-      h16* dst = &sKV[STAT ? 0 : buf][isv][pc * 512];
-      if (STAT && buf == 1) dst = &sKV1[isv][pc * 512];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)dst, 16, (int)voff[j], (int)(kt * SA_KT * ld * 2), 0, 0);
-    }
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  // slot as a compile-time constant (the unrolled loop) or a run-time int (the tiles outside it)
+  auto slot_ptr = [&](auto sl, int isv) -> h16* {
+    if constexpr (std::is_same<decltype(sl), int>::value) return sl ? sKV1[isv] : sKV0[isv];
+    else return decltype(sl)::value == 0 ? sKV0[isv] : sKV1[isv];
   };
-  // STAT: the same with the slot a compile-time constant (the unrolled loop's DMA)
-  auto dma_s = [&](int kt, auto slot_tag) {
-    constexpr int SL = decltype(slot_tag)::value;
+  auto dma = [&](int kt, auto sl) {  // tile kt -> ring slot sl (= kt & 1)
 #pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int gp = wave * PPW + j, isv = gp >> 3, pc = gp & 7;
-      h16* dst = SL == 0 ? &sKV[0][isv][pc * 512] : &sKV1[isv][pc * 512];
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)dst, 16, (int)voff[j], (int)(kt * SA_KT * ld * 2), 0, 0);
+    for (int j = 0; j < 4; ++j) {
+      const int gp = wave * 4 + j, isv = gp >> 3, pc = gp & 7;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(krs, (VDA_LDS void*)(slot_ptr(sl, isv) + pc * 512), 16, (int)voff[j],
+                                               (int)(kt * SA_KT * ld * 2), 0, 0);
     }
   };
 
@@ -350,8 +314,8 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
 
   // Lane-constant LDS byte offsets: K fragment ks of key row r32 (key block kb adds 32 rows = 4 KiB),
   // transposed-V read base of output tile dt (key slice ps adds 16 rows = 2 KiB, the second read of
-  // a fragment 8 rows = 1 KiB).  The swizzle terms depend on the lane only, so per tile the reads
-  // cost one address add per ks / dt and the rest are immediate offsets.
+  // a fragment 8 rows = 1 KiB).  The swizzle terms depend on the lane only, so the reads cost one
+  // address add per ks / dt and the rest are immediate offsets.
   unsigned kofs[4], vofs[2];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) kofs[ks] = (unsigned)sa_kslot(r32, ks * 2 + hf) * 16u;
@@ -361,250 +325,115 @@ __global__ __launch_bounds__(64 * NW, WPE) void spatial_attn32_kernel(const h16*
     vofs[dt] = (unsigned)(sa_vslot(r0, col >> 3) * 8 + (col & 7)) * 2u;
   }
   // Deferred re-base (FA-style online softmax without a per-tile max): P = exp2(S - m) against the
-  // running reference m; a tile only re-bases when a lane's P sum passes 2^15 (then some P may not
-  // fit fp16: the scores are recomputed, the true tile max taken and the tile redone), so the steady
-  // state computes no max at all.  P <= 2^15 keeps P exact to fp16 rounding and the fp32 sums far
-  // from overflow.
-  auto tile = [&](int kt, auto first_tag, auto mask_tag, auto slot_tag) {
+  // running reference m; a half only re-bases when a lane's P sum passes 2^15 (then some P may not fit
+  // fp16: the scores are recomputed, the true max taken and the half redone), so the steady state
+  // computes no max at all.  P <= 2^15 keeps P exact to fp16 rounding and the fp32 sums far from
+  // overflow.  The first half of the first tile always re-bases (m starts at 0, not at a real max).
+  auto tile = [&](int kt, auto first_tag, auto mask_tag, auto sl) {
     constexpr bool FIRST = decltype(first_tag)::value;
     constexpr bool MASK = decltype(mask_tag)::value;
-    constexpr int SL = decltype(slot_tag)::value;  // STAT: the tile's slot (-1: from kt)
-    // ring slot byte offset through an opaque scalar move: the compiler would otherwise strength-reduce
-    // kt % 3 into per-read address updates (two VALU per read)
-    const char* kbase;
-    const char* vbase;
-    if constexpr (SL >= 0) {
-      kbase = reinterpret_cast<const char*>(SL == 0 ? sKV[0][0] : sKV1[0]);
-      vbase = reinterpret_cast<const char*>(SL == 0 ? sKV[0][1] : sKV1[1]);
-    } else if constexpr (STAT) {
-      kbase = reinterpret_cast<const char*>((kt & 1) ? sKV1[0] : sKV[0][0]);
-      vbase = reinterpret_cast<const char*>((kt & 1) ? sKV1[1] : sKV[0][1]);
-    } else {
-      unsigned bo;
-      asm volatile("s_mul_i32 %0, %1, %2" : "=s"(bo) : "s"(kt % NBUF), "n"(2 * SA_KT * SD * 2));
-      kbase = reinterpret_cast<const char*>(sKV[0][0]) + bo;
-      vbase = reinterpret_cast<const char*>(sKV[0][1]) + bo;
-    }
-    if constexpr (HALF) {
-      // the softmax unit is a 32-key half of the tile (key block kb): its 4 QK MFMAs, 16 exponentials
-      // and 4 PV MFMAs, with half the score / P registers live
+    const char* kbase = reinterpret_cast<const char*>(slot_ptr(sl, 0));
+    const char* vbase = reinterpret_cast<const char*>(slot_ptr(sl, 1));
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        f16x s1;
-        auto qk1 = [&]() {
-          if (SA_KPRE) {  // the half's 4 K fragments requested together, then the MFMA chain
-            h8 kf[4];
+    for (int kb = 0; kb < 2; ++kb) {
+      f16x s1;
+      auto qk = [&]() {
 #pragma unroll
-            for (int ks = 0; ks < 4; ++ks) kf[ks] = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) s1 = mfma32(kf[ks], qf[ks], ks == 0 ? negm : s1);
-          } else {
-#pragma unroll
-          for (int ks = 0; ks < 4; ++ks) {
-            const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
-            s1 = mfma32(kf, qf[ks], ks == 0 ? negm : s1);
-          }
-          }
-          if constexpr (MASK) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-              if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) s1[r] = -INFINITY;
-          }
-        };
-        auto max1 = [&]() {
-          float mx = fmaxf(fmaxf(s1[0], s1[1]), s1[2]);
-#pragma unroll
-          for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s1[r]), s1[r + 1]);
-          mx = fmaxf(mx, s1[15]);
-          return half_max(mx);
-        };
-        auto rebase1 = [&](float sh) {
-          mrun += sh;
-#pragma unroll
-          for (int r = 0; r < 16; ++r) negm[r] = -mrun;
-          s1 -= sh;
-        };
-        h8 p2[2];
-        float tt;
-        auto expo1 = [&]() {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float pv = __builtin_amdgcn_exp2f(s1[r]);
-            if (!SA_DOT2) tt = r == 0 ? pv : tt + pv;  // (no add of 0 to start the chain)
-            p2[r >> 3][r & 7] = (h16)pv;
-          }
-          if (SA_DOT2) tt = sa_psum(p2[1], sa_psum(p2[0], 0.f));
-        };
-        if (SA_PRIO) __builtin_amdgcn_s_setprio(1);
-        qk1();
-        if (SA_PRIO) __builtin_amdgcn_s_setprio(0);
-        if (FIRST && kb == 0) {
-          rebase1(max1());
-          expo1();
-        } else {
-          expo1();
-          if (__any(!(tt <= 32768.f))) {  // rare: re-base this half on its true max and redo it
-            qk1();
-            const float sh = fmaxf(max1(), 0.f);
-            const float alpha = __builtin_amdgcn_exp2f(-sh);
-            lsum *= alpha;
-            o[0] *= alpha;
-            o[1] *= alpha;
-            rebase1(sh);
-            expo1();
-          }
-        }
-        lsum += tt;
-        if (SA_PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int ps = 0; ps < 2; ++ps) {
-#pragma unroll
-          for (int dt = 0; dt < 2; ++dt) {
-            const char* va = vbase + vofs[dt] + (kb * 2 + ps) * 2048;
-            const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
-            const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
-            const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-            o[dt] = mfma32(vf, p2[ps], o[dt]);
-          }
-        }
-        if (SA_PRIO) __builtin_amdgcn_s_setprio(0);
-      }
-      return;
-    }
-    f16x sc[2];
-    auto qk = [&]() {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {  // the two key blocks' accumulation chains interleaved
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+        for (int ks = 0; ks < 4; ++ks) {
           const h8 kf = *reinterpret_cast<const h8*>(kbase + kofs[ks] + kb * 4096);
-          sc[kb] = mfma32(kf, qf[ks], ks == 0 ? negm : sc[kb]);
+          s1 = mfma32(kf, qf[ks], ks == 0 ? negm : s1);
         }
-      }
-      if constexpr (MASK) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+        if constexpr (MASK) {
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) sc[kb][r] = -INFINITY;
-      }
-    };
-    qk();
-    auto tile_max = [&]() {
-      float mx = fmaxf(fmaxf(sc[0][0], sc[0][1]), sc[0][2]);
+            if (kt * SA_KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hf >= N) s1[r] = -INFINITY;
+        }
+      };
+      auto smax = [&]() {
+        float mx = fmaxf(fmaxf(s1[0], s1[1]), s1[2]);
 #pragma unroll
-      for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[0][r]), sc[0][r + 1]);
-      mx = fmaxf(fmaxf(mx, sc[0][15]), sc[1][0]);
+        for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, s1[r]), s1[r + 1]);
+        mx = fmaxf(mx, s1[15]);
+        return half_max(mx);
+      };
+      auto rebase = [&](float sh) {
+        mrun += sh;
 #pragma unroll
-      for (int r = 1; r < 15; r += 2) mx = fmaxf(fmaxf(mx, sc[1][r]), sc[1][r + 1]);
-      mx = fmaxf(mx, sc[1][15]);
-      return half_max(mx);
-    };
-    auto rebase = [&](float sh) {
-      mrun += sh;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) negm[r] = -mrun;
-      sc[0] -= sh;
-      sc[1] -= sh;
-    };
-    h8 pf[4];
-    float t0, t1;
-    auto expo = [&]() {
-      t0 = 0.f;
-      t1 = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+        for (int r = 0; r < 16; ++r) negm[r] = -mrun;
+        s1 -= sh;
+      };
+      h8 pf[2];
+      float tt;
+      auto expo = [&]() {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(sc[kb][r]);
-          if (!SA_DOT2) {
-            if (kb == 0) t0 += pv;
-            else t1 += pv;
-          }
-          pf[kb * 2 + (r >> 3)][r & 7] = (h16)pv;
+          const float pv = __builtin_amdgcn_exp2f(s1[r]);
+          tt = r == 0 ? pv : tt + pv;  // (no add of 0 to start the chain)
+          pf[r >> 3][r & 7] = (h16)pv;
         }
-      if (SA_DOT2) {
-        t0 = sa_psum(pf[1], sa_psum(pf[0], 0.f));
-        t1 = sa_psum(pf[3], sa_psum(pf[2], 0.f));
-      }
-    };
-    if constexpr (FIRST) {
-      rebase(tile_max());
-      expo();
-    } else {
-      expo();
-      if (__any(!(t0 + t1 <= 32768.f))) {  // rare: re-base on the true tile max and redo the tile
-        qk();  // the scores again (the K slot is still resident): they need not stay live past expo
-        const float sh = fmaxf(tile_max(), 0.f);
-        const float alpha = __builtin_amdgcn_exp2f(-sh);
-        lsum *= alpha;
-        o[0] *= alpha;
-        o[1] *= alpha;
-        rebase(sh);
+      };
+      __builtin_amdgcn_s_setprio(1);
+      qk();
+      __builtin_amdgcn_s_setprio(0);
+      if (FIRST && kb == 0) {
+        rebase(smax());
         expo();
+      } else {
+        expo();
+        if (__any(!(tt <= 32768.f))) {  // rare: re-base this half on its true max and redo it
+          qk();  // the scores again (the K slot is still resident): they need not stay live past expo
+          const float sh = fmaxf(smax(), 0.f);
+          const float alpha = __builtin_amdgcn_exp2f(-sh);
+          lsum *= alpha;
+          o[0] *= alpha;
+          o[1] *= alpha;
+          rebase(sh);
+          expo();
+        }
       }
-    }
-    lsum += t0 + t1;
+      lsum += tt;
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int ps = 0; ps < 4; ++ps) {  // the two output tiles' chains interleaved
+      for (int ps = 0; ps < 2; ++ps) {  // the two output tiles' chains interleaved
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const char* va = vbase + vofs[dt] + ps * 2048;
-        const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
-        const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
-        const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-        o[dt] = mfma32(vf, pf[ps], o[dt]);
+        for (int dt = 0; dt < 2; ++dt) {
+          const char* va = vbase + vofs[dt] + (kb * 2 + ps) * 2048;
+          const h4 v0 = lds_read_tr16(reinterpret_cast<const h16*>(va));
+          const h4 v1 = lds_read_tr16(reinterpret_cast<const h16*>(va + 1024));
+          const h8 vf = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+          o[dt] = mfma32(vf, pf[ps], o[dt]);
+        }
       }
+      __builtin_amdgcn_s_setprio(0);
     }
   };
   const int ntiles = (N + SA_KT - 1) / SA_KT;
-  auto enter = [&](int kt) {  // tile kt landed and visible; ring slot of kt-1 free -> prefetch kt+NBUF-1
-    // this wave's DMA issued after tile kt's: tiles kt+1 .. min(kt+NBUF-2, ntiles-1), PPW pieces each
-    const int later = min(NBUF - 2, ntiles - 1 - kt);
-    if (later <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if (later * PPW == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else if (later * PPW == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (later * PPW == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  // tile kt landed and visible (its DMA is this wave's only one in flight), and every wave is done with
+  // tile kt - 1: its slot takes tile kt + 1
+  auto enter = [&](int kt, auto next_slot) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), as the builtin: hipcc's own wait bookkeeping sees it
     __builtin_amdgcn_s_barrier();
-    if (kt + NBUF - 1 < ntiles) dma(kt + NBUF - 1);
+    if (kt + 1 < ntiles) dma(kt + 1, next_slot);
   };
-#pragma unroll
-  for (int i = 0; i < NBUF - 1; ++i)
-    if (i < ntiles) dma(i);
+  // a tile whose slot is only known at run time (the first, an odd leftover and the partial last one)
+  auto tile_any = [&](int kt, auto first_tag, auto mask_tag) {
+    enter(kt, (kt + 1) & 1);
+    tile(kt, first_tag, mask_tag, kt & 1);
+  };
+  dma(0, S0{});
   const bool tail = N % SA_KT != 0;
-  using dyn_slot = std::integral_constant<int, -1>;
-  enter(0);
-  if (ntiles == 1 && tail) tile(0, std::true_type{}, std::true_type{}, dyn_slot{});
-  else tile(0, std::true_type{}, std::false_type{}, dyn_slot{});
+  if (ntiles == 1 && tail) tile_any(0, std::true_type{}, std::true_type{});
+  else tile_any(0, std::true_type{}, std::false_type{});
   const int nfull = ntiles - (tail ? 1 : 0);
   int kt = 1;
-  if constexpr (STAT) {
-    // pairs (odd kt in slot 1, even kt + 1 in slot 0); enter() of each issues the next tile's DMA into
-    // the slot the previous tile read
-    using s0 = std::integral_constant<int, 0>;
-    using s1 = std::integral_constant<int, 1>;
-    auto enter_s = [&](int k, auto next_slot) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile k landed (NBUF 2: no newer pieces in flight)
-      __builtin_amdgcn_s_barrier();
-      if (k + 1 < ntiles) dma_s(k + 1, next_slot);
-    };
-    for (; kt + 1 < nfull; kt += 2) {
-      enter_s(kt, s0{});
-      tile(kt, std::false_type{}, std::false_type{}, s1{});
-      enter_s(kt + 1, s1{});
-      tile(kt + 1, std::false_type{}, std::false_type{}, s0{});
-    }
+  for (; kt + 1 < nfull; kt += 2) {  // pairs: odd kt in slot 1, even kt + 1 in slot 0
+    enter(kt, S0{});
+    tile(kt, std::false_type{}, std::false_type{}, S1{});
+    enter(kt + 1, S1{});
+    tile(kt + 1, std::false_type{}, std::false_type{}, S0{});
   }
-  for (; kt < nfull; ++kt) {
-    enter(kt);
-    tile(kt, std::false_type{}, std::false_type{}, dyn_slot{});
-  }
-  if (tail && ntiles > 1) {
-    enter(ntiles - 1);
-    tile(ntiles - 1, std::false_type{}, std::true_type{}, dyn_slot{});
-  }
+  if (kt < nfull) tile_any(kt, std::false_type{}, std::false_type{});
+  if (tail && ntiles > 1) tile_any(ntiles - 1, std::false_type{}, std::true_type{});
   // epilogue: lane holds Oᵀ[d = dt*32 + 8gq + 4hf + r][q]
   const float inv = 1.f / half_sum(lsum);
   if (q < N) {
@@ -893,11 +722,11 @@ extern "C" int vda_spatial_attention(const void* qkv, void* out, int32_t B, int3
     hipLaunchKernelGGL(spatial_attn_kernel, grid, dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
                        (h16*)out, N, H, scale * 1.4426950408889634f);
   } else {
-    const int nqb = (N + 32 * SA_NW - 1) / (32 * SA_NW);
+    const int nqb = (N + 127) / 128;
     const long nb = (long)nqb * H * B;
     VDA_CHECK_ARG(nb < 0x7fffffffL, "attention grid too large");
-    hipLaunchKernelGGL((spatial_attn32_kernel<SA_NW, SA_NBUF, SA_WPE, (bool)SA_HALF>), dim3((unsigned)nb), dim3(64 * SA_NW), 0,
-                       (hipStream_t)stream, (const h16*)qkv, (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
+    hipLaunchKernelGGL(spatial_attn32_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, (const h16*)qkv,
+                       (h16*)out, N, H, nqb, (int)nb, scale * 1.4426950408889634f);
   }
   VDA_LAUNCH_CHECK();
   return 0;

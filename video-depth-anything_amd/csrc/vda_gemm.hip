@@ -169,23 +169,27 @@ struct ConvLoader {
 };
 
 // ---- epilogue ------------------------------------------------------------------------------
+// LayerNorm folded into the GEMM (vda_epilogue.ln_stats / ln_colsum): the row's (mean, rstd), from
+// [M, 2] as is or from [M, ln_parts, 2] partial (sum, sumsq) over ln_parts column blocks
+__device__ __forceinline__ float2 epi_ln_row(const GemmParams& p, int m) {
+  const vda_epilogue& e = p.epi;
+  if (e.ln_parts > 0) {
+    float sm = 0.f, sq = 0.f;
+    for (int t = 0; t < e.ln_parts; ++t) {
+      const float2 pq = *reinterpret_cast<const float2*>(e.ln_stats + 2L * ((long)m * e.ln_parts + t));
+      sm += pq.x;
+      sq += pq.y;
+    }
+    const float mean = sm / (float)p.K;
+    return make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq / (float)p.K), 0.f) + e.ln_eps));
+  }
+  return *reinterpret_cast<const float2*>(e.ln_stats + 2L * m);
+}
 template <int ACT>
 __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4 v) {
   const vda_epilogue& e = p.epi;
   if (e.ln_stats) {  // LayerNorm folded into the GEMM: rstd * (acc - mean * colsum)
-    float2 mr;
-    if (e.ln_parts > 0) {  // partial (sum, sumsq) over ln_parts column blocks
-      float sm = 0.f, sq = 0.f;
-      for (int t = 0; t < e.ln_parts; ++t) {
-        const float2 pq = *reinterpret_cast<const float2*>(e.ln_stats + 2L * ((long)m * e.ln_parts + t));
-        sm += pq.x;
-        sq += pq.y;
-      }
-      const float mean = sm / (float)p.K;
-      mr = make_float2(mean, rsqrtf(fmaxf(fmaf(-mean, mean, sq / (float)p.K), 0.f) + e.ln_eps));
-    } else {
-      mr = *reinterpret_cast<const float2*>(e.ln_stats + 2L * m);
-    }
+    const float2 mr = epi_ln_row(p, m);
     const f4 c1 = *reinterpret_cast<const f4*>(e.ln_colsum + n);
 #pragma unroll
     for (int j = 0; j < 4; ++j) v[j] = mr.y * fmaf(-mr.x, c1[j], v[j]);
@@ -244,6 +248,15 @@ __device__ __forceinline__ void epi_store4(const GemmParams& p, int m, int n, f4
 __device__ __forceinline__ void epi_geglu4(const GemmParams& p, int m, int nh, int ng, int n_out,
                                            f4 vh, f4 vg) {
   const vda_epilogue& e = p.epi;
+  if (e.ln_stats) {  // LayerNorm folded in (the motion modules' ff_norm), on both halves before the gate
+    const float2 mr = epi_ln_row(p, m);
+    const f4 ch = *reinterpret_cast<const f4*>(e.ln_colsum + nh), cg = *reinterpret_cast<const f4*>(e.ln_colsum + ng);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      vh[j] = mr.y * fmaf(-mr.x, ch[j], vh[j]);
+      vg[j] = mr.y * fmaf(-mr.x, cg[j], vg[j]);
+    }
+  }
   if (e.bias) {
     vh += *reinterpret_cast<const f4*>(e.bias + nh);
     vg += *reinterpret_cast<const f4*>(e.bias + ng);
@@ -1934,6 +1947,13 @@ void launch_phased(const GemmParams& p, hipStream_t st) {
       return;
     }
   }
+  if constexpr (!CONV && XR == 2 && ACT == VDA_ACT_GEGLU) {
+    if (p.epi.ln_stats) {  // LN fold + GEGLU (the motion modules' ff_norm -> ff.net[0]), staged epilogue
+      hipLaunchKernelGGL((gemm256_kernel<XR, WR, CONV, ACT, false, true>), dim3(grid), dim3(512), 0, st, p, tiles_m, tiles_n,
+                         ticks, g_desync);
+      return;
+    }
+  }
   if constexpr (!CONV && XR == 2 && (ACT == VDA_ACT_NONE || ACT == VDA_ACT_GELU)) {
     const vda_epilogue& e = p.epi;
     const bool rows1 = e.store == VDA_STORE_ROWS && e.bias && !e.gamma && !e.res2 && !e.rowbias;
@@ -2061,12 +2081,12 @@ int check_epi(const vda_epilogue& e, int M, int N) {
                 (e.store == VDA_STORE_PIXEL_SHUFFLE && e.ps_k > 0 && e.ps_cout > 0 && e.ps_cout % 4 == 0 &&
                  e.ps_hin > 0 && e.ps_win > 0 && N == e.ps_k * e.ps_k * e.ps_cout && !e.res && !e.res2),
                 "bad pixel-shuffle store geometry");
-  // the LN fold exists for the activation-free and GELU epilogues (every kernel route applies it
+  // the LN fold exists for the activation-free, GELU and GEGLU epilogues (every kernel route applies it
   // there; anything else would silently run an un-normalised GEMM); with a row bias only on the
   // phased route's EK 3 epilogue (vda_gemm checks the shape)
   VDA_CHECK_ARG(!e.ln_stats || (e.ln_colsum && e.store == VDA_STORE_ROWS && !e.gamma &&
-                                 (e.act == VDA_ACT_NONE || e.act == VDA_ACT_GELU)),
-                "ln_stats needs ln_colsum, a row store, no gamma, activation none / gelu");
+                                 (e.act == VDA_ACT_NONE || e.act == VDA_ACT_GELU || e.act == VDA_ACT_GEGLU)),
+                "ln_stats needs ln_colsum, a row store, no gamma, activation none / gelu / geglu");
   VDA_CHECK_ARG(!e.ln_stats || !e.rowbias ||
                     (e.act == VDA_ACT_NONE && e.bias && !e.res && !e.res2 && !e.stats_out && e.rdiv >= 256),
                 "ln_stats with rowbias needs a bias, no activation / residual / stats_out, rdiv >= 256");

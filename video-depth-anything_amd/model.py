@@ -237,13 +237,15 @@ class VideoDepthAnything(nn.Module):
     of the packed-weight cache key): ``fold_layernorms`` folds the encoder's norm1 / norm2 into the
     qkv / fc1 GEMMs and the motion modules' attention-block LayerNorms into their q/k/v GEMMs (fp16
     mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
-    proj / fc2 epilogues instead of a separate pass, ``dynamic_tiles`` lets the encoder's persistent GEMMs
+    proj / fc2 epilogues instead of a separate pass, ``fold_ff_norm`` folds the motion modules' ff_norm into
+    their GEGLU GEMM (fp16 mode, with ``fold_layernorms``), ``dynamic_tiles`` lets the encoder's persistent GEMMs
     take their tiles by atomic ticket (per-stream counters, ``ops.sched_counters``) instead of a fixed
     stride.  No environment variable changes the schedule."""
 
     fold_layernorms: bool = True
     epilogue_stats: bool = True
     dynamic_tiles: bool = False
+    fold_ff_norm: bool = False  # built and tested; same-box forward A/B 693.7 -> 690.0 frames/s (r06_ab_ffold.log)
 
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
@@ -421,6 +423,15 @@ class VideoDepthAnything(nn.Module):
             q.ffnw, q.ffnb = _f(blk.ff_norm.weight).to(dev), _f(blk.ff_norm.bias).to(dev)
             q.ff1_w = _h(_geglu_interleave(blk.ff.net[0].proj.weight)).to(dev)
             q.ff1_b = _f(_geglu_interleave(blk.ff.net[0].proj.bias)).to(dev)
+            # ff_norm folded into the GEGLU GEMM (fp16): W' = gamma (.) W (rows interleaved as ff1_w), colsum
+            # of the fp16 W', b' = W beta + b; the statistics come from the last to_out GEMM's epilogue
+            q.fffold = not fp32 and bool(self.fold_layernorms)  # (the forward also checks fold_ff_norm)
+            if q.fffold:
+                w1 = blk.ff.net[0].proj.weight.detach().float()
+                q.ff1_wg = _geglu_interleave(w1 * blk.ff_norm.weight.detach().float()[None, :]).half().contiguous().to(dev)
+                q.ff1_cs = q.ff1_wg.float().sum(1).contiguous()
+                q.ff1_bb = _geglu_interleave(w1 @ blk.ff_norm.bias.detach().float()
+                                             + blk.ff.net[0].proj.bias.detach().float()).contiguous().to(dev)
             q.ff2_w, q.ff2_b = _h(blk.ff.net[2].weight).to(dev), _f(blk.ff.net[2].bias).to(dev)
             P.mm.append(q)
         self._packed[key] = P
@@ -465,13 +476,15 @@ class VideoDepthAnything(nn.Module):
     def _temporal(self, q: _Packed, x: torch.Tensor, B: int, T: int, S: int) -> torch.Tensor:
         """TemporalModule on token-major frames x [B*T*S, C] (motion_module.py:64-133).
         The attention blocks' LayerNorms (motion_module.py:175) are folded into their q/k/v GEMMs when
-        a frame spans >= 256 rows (each 256-row tile then sees <= 2 PE rows): the GEMM producing the
-        residual stream h (proj_in, then each to_out) writes h's per-row partial sums."""
+        a frame spans >= 256 rows (each 256-row tile then sees <= 2 PE rows), and ff_norm (:182) into the
+        GEGLU GEMM: the GEMM producing the residual stream h (proj_in, then each to_out) writes h's
+        per-row partial sums."""
         C = q.C
         M = x.shape[0]
         xn = ops.groupnorm(x, q.gnw, q.gnb, B * T, 32, 1e-6)
         fold = [a.fold and S >= 256 and M >= 4096 for a in q.attn]
-        st = torch.empty(M + 1, (C + 255) // 256, 2, device=x.device) if any(fold) else None
+        fffold = q.fffold and bool(self.fold_ff_norm)
+        st = torch.empty(M + 1, (C + 255) // 256, 2, device=x.device) if any(fold) or fffold else None
         h = ops.gemm(xn, q.pin_w, bias=q.pin_b, stats_out=st if fold[0] else None)
         for i, a in enumerate(q.attn):
             if fold[i]:  # rstd (h W'^T - mean colsum) + W beta + pe[t] W^T
@@ -486,10 +499,16 @@ class VideoDepthAnything(nn.Module):
                 else:  # pe='rope': rotary q/k (theta 1e4, pairs over all C channels) in the attention kernel
                     qkv = ops.gemm(n, a.qkv_w)
                     at = ops.temporal_attention(qkv, B, T, S, 8, C // 8, rope_theta=10000.0)
-            nxt = i + 1 < len(q.attn) and fold[i + 1]
+            # the residual-stream GEMM writes the row statistics of h for the next folded LayerNorm: the
+            # next attention block's (when folded), after the last block the feed-forward's ff_norm
+            nxt = fold[i + 1] if i + 1 < len(q.attn) else fffold
             h = ops.gemm(at, a.out_w, bias=a.out_b, res=h, out=h, stats_out=st if nxt else None)
-        n = ops.layernorm(h, q.ffnw, q.ffnb, 1e-5)
-        g = ops.gemm(n, q.ff1_w, bias=q.ff1_b, act=ACT_GEGLU)
+        if fffold:  # rstd (h W'^T - mean colsum) + W beta + b, then the GEGLU gate (attention.py:363-384)
+            g = ops.gemm(h, q.ff1_wg, bias=q.ff1_bb, act=ACT_GEGLU, ln_stats=st, ln_parts=st.shape[1], ln_eps=1e-5,
+                         ln_colsum=q.ff1_cs)
+        else:
+            n = ops.layernorm(h, q.ffnw, q.ffnb, 1e-5)
+            g = ops.gemm(n, q.ff1_w, bias=q.ff1_b, act=ACT_GEGLU)
         h = ops.gemm(g, q.ff2_w, bias=q.ff2_b, res=h, out=h)
         return ops.gemm(h, q.pout_w, bias=q.pout_b, res=x)
 
