@@ -50,7 +50,7 @@ sys.path.insert(0, REPO)
 PEAK_FP16_TFLOPS = 2500.0  # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
 REF_A100_FPS = 71.4        # README.md:52-61 ViT-L fp16 14 ms/frame on 1x A100
 GFLOP_PER_FRAME = {("vitl", 518, 518): 1404.6, ("vits", 518, 518): 121.3, ("vitl", 518, 924): 2761.5}
-PROFILE_ROUND = "r05"      # profiles/<round>_pmc_*.json carry the PMC figures quoted in the line
+PROFILE_ROUND = "r06"      # profiles/<round>_pmc_*.json carry the PMC figures quoted in the line
 
 
 def parse():
