@@ -360,12 +360,20 @@ def roofline(model, launches, pmc_ok=True):
     mm = (pmc("pmc_mfma") or {}) if pmc_ok else {}
     mfma_busy = next((e.get("mfma_busy") for e in mm.get("kernels", {}).values() if e.get("tag") == "enc_fc1"), None)
     src = lambda name, d: f"profiles/{PROFILE_ROUND}_{name}.json" if d else None
+    # the shader clock fc1 holds under load, measured in-kernel (s_memtime / s_memrealtime stamps of a
+    # -DVDA_TS build, tools/clock_probe.py): the 2.5 PF peak is rated at 2.4 GHz, so frac_at_held_clock is
+    # the same launch against the peak at the clock the chip actually sustains (not measured by this run)
+    ck = (pmc("clock_probe") or {}) if pmc_ok else {}
+    clk = ck.get("fc1_clock_ghz")
     return {"bound": "mfma", "achieved": round(achieved, 1), "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4), "traffic": f1.get("hbm_bytes_per_launch"),
             "mfma_busy_pmc": mfma_busy,
+            "clock_ghz_in_kernel": clk,
+            "frac_at_held_clock": round(achieved / (PEAK_FP16_TFLOPS * clk / 2.4), 4) if clk else None,
             # traffic and mfma_busy_pmc are NOT measured by this run: they are read from the committed
             # rocprofv3 --pmc summaries named here (tools/pmc_fc1.py, tools/pmc_mfma_summary.py)
             "pmc_source": {"traffic": src("pmc_fc1", f1), "mfma_busy_pmc": src("pmc_mfma", mfma_busy is not None),
+                           "clock_ghz_in_kernel": src("clock_probe", clk),
                            "pmc_tag": "enc_fc1",
                            "note": None if pmc_ok else "the committed PMC summaries cover the ViT-L 32x518x518 "
                                                         "workload only; traffic / mfma_busy_pmc left null"},

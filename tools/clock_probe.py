@@ -24,6 +24,9 @@ L = ctypes.CDLL(os.path.abspath(sys.argv[1]))
 _lib._declare(L)
 P = ctypes.CDLL(os.path.abspath(sys.argv[2]))
 secs = float(sys.argv[3]) if len(sys.argv) > 3 else 2.5
+out_json = sys.argv[4] if len(sys.argv) > 4 else None  # optional: the medians as JSON (profiles/<round>_clock_probe.json)
+summary = {"method": "median over blocks of d(s_memtime) / d(s_memrealtime) x 100 MHz, last launch after back-to-back "
+                     "launches on random data (tools/clock_probe.py, -DVDA_TS build)"}
 for f in (L.vda_debug_clock_stamps, L.vda_debug_attn_clock_stamps):
     f.argtypes = [ctypes.c_void_p]
 P.probe_mfma_only.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -33,7 +36,7 @@ st = torch.cuda.current_stream().cuda_stream
 cus = torch.cuda.get_device_properties(0).multi_processor_count
 
 
-def run(name, launch, read, nblocks, flop=None):
+def run(name, launch, read, nblocks, flop=None, key=None):
     """launch() back to back for `secs`, then read the last launch's stamps."""
     launch()
     torch.cuda.synchronize()
@@ -61,6 +64,9 @@ def run(name, launch, read, nblocks, flop=None):
         line += (f"; {tf:7.1f} TF/s = {tf / 2500:.3f} of 2.5 PF, {tf / (2500 * np.median(ghz) / 2.4):.3f} of the "
                  f"peak at that clock")
     print(line, flush=True)
+    if key:
+        summary[key + "_clock_ghz"] = round(float(np.median(ghz)), 3)
+        summary[key + "_us"] = round(us, 1)
 
 
 torch.manual_seed(0)
@@ -90,7 +96,7 @@ def read_gemm():
     return buf
 
 
-run("fc1 GEMM (LN fold + GELU) 43840x4096x1024", gemm, read_gemm, cus, 2.0 * M * N * K)
+run("fc1 GEMM (LN fold + GELU) 43840x4096x1024", gemm, read_gemm, cus, 2.0 * M * N * K, key="fc1")
 
 B, Nt, H, D = 32, 1370, 16, 64
 qkv = (torch.randn(B * Nt, 3 * H * D, device=dev) * 1.5).half()
@@ -108,7 +114,8 @@ def read_attn():
 
 
 nqb = (Nt + 127) // 128
-run("spatial attention 32x1370x16x64", attn, read_attn, min(8192, B * H * nqb), 4.0 * B * H * Nt * Nt * D)
+run("spatial attention 32x1370x16x64", attn, read_attn, min(8192, B * H * nqb), 4.0 * B * H * Nt * Nt * D,
+    key="spatial_attention")
 
 ts = torch.zeros(cus * 4, dtype=torch.int64, device=dev)
 src = (torch.randn(64 << 20, device=dev)).half()  # 128 MiB of random fp16
@@ -125,7 +132,8 @@ def read_probe():
 
 
 # 8 waves x 8 MFMAs (16x16x32, 16 cycles each on one SIMD) per iteration
-run("probe: MFMA only (8 waves/CU, operands in registers)", mfma, read_probe, cus, 2.0 * 16 * 16 * 32 * 8 * 8 * iters * cus)
+run("probe: MFMA only (8 waves/CU, operands in registers)", mfma, read_probe, cus, 2.0 * 16 * 16 * 32 * 8 * 8 * iters * cus,
+    key="mfma_only_probe")
 steps = 2048
 src_bytes = 64 << 20
 
@@ -134,6 +142,8 @@ def dma():
     assert P.probe_dma_only(src.data_ptr(), src_bytes, ts.data_ptr(), cus, steps, st) == 0
 
 
-run("probe: LDS-DMA staging only (64 KiB per step, 2-slot ring)", dma, read_probe, cus)
-dt_us = None
+run("probe: LDS-DMA staging only (64 KiB per step, 2-slot ring)", dma, read_probe, cus, key="dma_only_probe")
 print(f"(dma probe: {steps} steps x 64 KiB per CU per launch)", flush=True)
+if out_json:
+    import json
+    json.dump(summary, open(out_json, "w"), indent=1)
