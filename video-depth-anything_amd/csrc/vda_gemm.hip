@@ -393,9 +393,6 @@ __global__ __launch_bounds__(256) void gemm_reg_kernel(GemmParams p, int tiles_n
 // GROUP_M m-panels at a time so co-resident blocks share X panels and W tiles in their XCD's L2.
 __device__ __attribute__((aligned(64))) uint4 g_zero_page[4];
 
-#ifndef VDA_RES_L2PF  // proj / fc2: the epilogue's residual tile fetched ahead by LDS-DMA into a scratch slot
-#define VDA_RES_L2PF 0   // during the last K steps, so its epilogue loads hit L2 / MALL (A/B builds)
-#endif
 #ifndef VDA_GROUP_M  // (A/B builds only)
 #define VDA_GROUP_M 8
 #endif
@@ -1123,27 +1120,6 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
   };
 
   unsigned tk = 0;  // dynamic schedule: the ticket in flight (wave 0, lane 0)
-  // residual prefetch (VDA_RES_L2PF): the staged epilogue's 16 residual loads per thread (rows row0 +
-  // 16 it, 16-B chunk q) issued as LDS-DMA pieces into a 1-KiB scratch slot per wave (the bytes are
-  // never read: the point is that the epilogue's own loads then hit L2 / the MALL instead of HBM, and
-  // that 256 CUs do not request their 128-KiB residual tiles in the same few microseconds)
-  constexpr bool L2PF = VDA_RES_L2PF && XR == 2 && WR == 2 && ACT == VDA_ACT_NONE && !CONV && !ROWB && !LNF && EK == 0;
-  bool pf_on = false;
-  int pf_pps = 1;
-  unsigned pf_vo = 0, pf_so = 0;
-  __amdgpu_buffer_rsrc_t pf_rs;
-  if constexpr (L2PF) {
-    pf_on = p.epi.res != nullptr && p.epi.res2 == nullptr && p.epi.store == VDA_STORE_ROWS && nk >= 10;
-    if (pf_on) {
-      pf_pps = nk - 2 >= 16 ? 1 : 2;
-      const long ld = p.epi.ldres, mrows = p.M - m0;
-      pf_rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const h16*)p.epi.res + (long)m0 * ld), (short)0,
-                                                (int)(mrows * ld * 2 < 0x7fffffffL ? mrows * ld * 2 : 0x7fffffffL), 0x00020000);
-      const int q = tid % (BN / 8), row0 = tid / (BN / 8), c = n0 + q * 8;
-      pf_vo = c < p.N ? (unsigned)(((long)row0 * ld + c) * 2) : 0x80000000u;
-      pf_so = (unsigned)((512 / (BN / 8)) * ld * 2);
-    }
-  }
   // One quarter is staged per phase, each >= 2 phases after its last read (WAR under the stagger)
   // and retired by the P4 wait one phase before its first read:
   //   P1: Xq1(t+1) -> other buffer   P2: Wq0(t+1) -> other   P3: Xq0(t+2) -> this   P4: Wq1(t+2) -> this
@@ -1168,29 +1144,11 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
     }
     if (more2) stage_x(kt + 2, cb, 0);
     mma(1, 1);
-    // P4: retire everything but this tile's two P3/P4 quarters (and this step's residual prefetch pieces)
+    // P4: retire everything but this tile's two P3/P4 quarters
     load_w(base, 0);
     if (more2) {
       stage_w(kt + 2, cb, 1);
-      int npf = 0;
-      if constexpr (L2PF) {
-        if (pf_on) {
-          // pieces j0 .. j0 + pf_pps - 1 of the 16 (the last ones at step nk - 3), one 1-KiB row group each
-          const int j0 = 16 - (nk - 2 - kt) * pf_pps;
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const int j = j0 + d;
-            if (d < pf_pps && j >= 0 && j < 16) {
-              __builtin_amdgcn_raw_ptr_buffer_load_lds(pf_rs, (VDA_LDS void*)(smem + 2 * BUF + wave * 512), 16, (int)pf_vo,
-                                                       j * (int)pf_so, 0, 0);
-              ++npf;
-            }
-          }
-        }
-      }
-      if (npf == 2) wait_vmcnt<XR + WR + 2>();
-      else if (npf == 1) wait_vmcnt<XR + WR + 1>();
-      else wait_vmcnt<XR + WR>();
+      wait_vmcnt<XR + WR>();
     } else {
       wait_vmcnt<0>();
     }
@@ -1830,9 +1788,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmParams p, int tiles_m,
   constexpr int BUF = (XR + WR) * 128 * BK;
   constexpr bool TAB = XR == 2 && (ACT == VDA_ACT_GELU || ACT == VDA_ACT_GEGLU);
   // + 64 halves at the end (XR 2): the dynamic schedule's successor slot
-  constexpr bool L2PF = VDA_RES_L2PF && XR == 2 && WR == 2 && ACT == VDA_ACT_NONE && !CONV && !ROWB && !LNF && EK == 0;
   constexpr int SMEM_HALVES = 2 * BUF + (TAB ? PHI_LDS_HALVES : 0) + (LNF ? 4096 + 1024 : 0) + (EK == 2 ? 4096 : 0) +
-                              (L2PF ? 4096 : 0) +
                               (EK == 3 ? 2048 : 0) + (XR == 2 ? 64 : 0);
   __shared__ __attribute__((aligned(1024))) h16 smem[SMEM_HALVES];
   const int ntiles = tiles_m * tiles_n;
