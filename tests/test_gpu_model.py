@@ -47,6 +47,28 @@ def test_forward_matches_oracle(enc, B, T, H, W):
     assert err <= TOL_FP16
 
 
+@pytest.mark.parametrize("enc,T,H,W", [("vits", 32, 266, 266), ("vitl", 6, 140, 196)])
+def test_forward_ff_norm_fold_matches_oracle(enc, T, H, W):
+    """The model switch fold_ff_norm (off by default: slower in the forward A/B) folds each motion module's
+    ff_norm into its GEGLU GEMM with statistics from the last to_out; the forward with it still meets the
+    bar against the oracle, and differs from the unfolded forward only by fp16 rounding."""
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(1, T, 3, H, W, generator=g)
+    m = model(enc)
+    d0 = m(x.cuda()).float().cpu()
+    m.fold_ff_norm = True
+    try:
+        d1 = m(x.cuda()).float().cpu()
+    finally:
+        m.fold_ff_norm = False
+    ref = vda_oracle.forward(recipe_state_dict(enc), enc, x)
+    err = rel_l1(d1, ref)
+    print(f"{enc} 1x{T}x{H}x{W} with fold_ff_norm: rel-L1 vs oracle = {err:.3e} (unfolded {rel_l1(d0, ref):.3e})")
+    assert err <= TOL_FP16
+    assert rel_l1(d1, d0) < 1e-3
+
+
 def test_forward_deterministic_and_batch_independent():
     """Clip-parallel sharding relies on per-clip independence: B=2 == two B=1 runs."""
     g = torch.Generator().manual_seed(3)
