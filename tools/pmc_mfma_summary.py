@@ -69,8 +69,9 @@ for d in disp.values():
     a["kernel_cycles"] += cyc
     a["grbm_cycles"] = a.get("grbm_cycles", 0.0) + d["GRBM_GUI_ACTIVE"] / 8.0
     a["ns"] += d.get("ns", 0)
-res = {"n_cu": n_cu, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 * n_cu * 4)", "kernels": {}}
-tot_b = tot_c = 0.0
+res = {"n_cu": n_cu, "formula": "SQ_VALU_MFMA_BUSY_CYCLES / (min(GRBM_GUI_ACTIVE/8, wall ns x 2.4) * n_cu * 4)",
+       "kernels": {}}
+tot_b = tot_c = tot_g = 0.0
 for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["kernel_cycles"]):
     busy = a["mfma_busy_cycles"] / max(1.0, a["kernel_cycles"] * n_cu * 4)
     e = {"tag": tag_of(k), "dispatches": a["dispatches"], "mfma_busy": round(busy, 4), "kernel_cycles": a["kernel_cycles"]}
@@ -81,9 +82,11 @@ for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["kernel_cycles"]):
     res["kernels"][k] = e
     tot_b += a["mfma_busy_cycles"]
     tot_c += a["kernel_cycles"]
+    tot_g += a.get("grbm_cycles", 0.0)
 res["all_kernels_mfma_busy"] = round(tot_b / max(1.0, tot_c * n_cu * 4), 4)
+res["all_kernels_mfma_busy_uncapped"] = round(tot_b / max(1.0, tot_g * n_cu * 4), 4)  # GRBM/8 cycles (rounds <= 5)
 json.dump(res, open(out, "w"), indent=1)
 for k, e in list(res["kernels"].items())[:14]:
     clk = e.get("clock_ghz")
     print(f"{e['mfma_busy']:7.3f}  {clk if clk is not None else '  -  '} GHz  {e['dispatches']:5d}  {k}")
-print("all kernels", res["all_kernels_mfma_busy"])
+print("all kernels", res["all_kernels_mfma_busy"], "(uncapped GRBM cycles:", res["all_kernels_mfma_busy_uncapped"], ")")
