@@ -175,6 +175,25 @@ int vda_groupnorm(const void* x, void* y, const float* gamma, const float* beta,
 int64_t vda_groupnorm_workspace(int32_t F, int32_t S, int32_t C, int32_t groups);
 
 /*
+ * GroupNorm -> Linear: Y [F*S, N] = GN(X) · Wᵀ + bias, X [F, S, C] half, W [N, C] half, gamma / beta /
+ * bias fp32 (bias may be NULL), Y half.  Replaces motion_module.py:116-119 (self.norm(hidden_states),
+ * the (b f) c h w -> (b f) (h w) c rearrange, self.proj_in) - the op SURVEY.md §8(b) names
+ * groupnorm_linear.  For groups == 32 and N == C in {64, 128, 256} (every motion module of the
+ * shipped encoders) the normalisation is applied to the GEMM operand in registers (no normalised copy
+ * of X in HBM): W' = fp16(W diag(gamma)) and W beta + bias are formed per block in LDS, and the operand
+ * is fp16((x - mean) rstd); other shapes run vda_groupnorm + vda_gemm through the workspace
+ * (vda_groupnorm_linear_fused says which; ViT-L's C = 1024 modules take this route).  stats_out
+ * (optional): [F*S, ceil(N / 256), 2] per-row (sum, sum of squares) of the stored fp16 rows over
+ * 256-column blocks, as vda_epilogue.stats_out.  ws: a 16-byte aligned
+ * device buffer of at least vda_groupnorm_linear_workspace(...) bytes.  x, w, y 16-byte aligned.
+ */
+int vda_groupnorm_linear(const void* x, const float* gamma, const float* beta, int32_t F, int32_t S,
+                         int32_t C, int32_t groups, float eps, const void* w, const float* bias, void* y,
+                         int32_t N, float* stats_out, void* ws, int64_t ws_bytes, void* stream);
+int64_t vda_groupnorm_linear_workspace(int32_t F, int32_t S, int32_t C, int32_t groups, int32_t N);
+int vda_groupnorm_linear_fused(int32_t C, int32_t groups, int32_t N);
+
+/*
  * Spatial multi-head self-attention (flash / online softmax, fp16 MFMA, fp32 softmax).
  * qkv [B*N, 3*H*D] half laid out as [B, N, 3, H, D] (the nn.Linear qkv output);
  * out [B*N, H*D] half.  D must be 64.  Replaces dinov2_layers/attention.py:49-62/:65-81

@@ -174,6 +174,8 @@ def test_torch_ops_registered_meta_shapes_and_no_cpu_kernel():
     assert up.shape == (2, 20, 24, 32)
     o = torch.empty(100, 96, device="meta", dtype=torch.float16)
     assert torch.ops.vda.gemm.out(x, w, act=0, out=o) is not None
+    g = x.new_empty(64, dtype=torch.float32)
+    assert torch.ops.vda.groupnorm_linear(x, g, g, 4, 32, 1e-6, w, None).shape == (100, 96)
     with pytest.raises(NotImplementedError):
         torch.ops.vda.upsample_bilinear(torch.zeros(1, 2, 2, 8, dtype=torch.float16), 4, 4)
 
@@ -193,3 +195,33 @@ def test_workspace_queries():
     assert lib.vda_depth_head_workspace(32, 296, 296, 128, 518, 518) == 0   # fused resize: none
     assert lib.vda_depth_head_workspace(2, 20, 20, 32, 518, 518) == 0   # C % 32: fused depth conv
     assert lib.vda_depth_head_workspace(2, 20, 20, 40, 518, 518) == 2 * 518 * 518 * 40 * 2  # C % 32 != 0: materialised
+
+
+def test_groupnorm_linear_routes_and_validation():
+    """vda_groupnorm_linear (motion_module.py:116-119): the fused kernel serves groups 32 with N = C in
+    {64, 128, 256}; every other shape runs GroupNorm + GEMM through the workspace, which then also holds
+    the normalised copy of x.  Invalid arguments return -22 before any launch."""
+    lib = _lib.lib()
+    for C in (64, 128, 256):
+        assert lib.vda_groupnorm_linear_fused(C, 32, C) == 1
+    assert lib.vda_groupnorm_linear_fused(256, 32, 512) == 0
+    assert lib.vda_groupnorm_linear_fused(256, 16, 256) == 0
+    assert lib.vda_groupnorm_linear_fused(512, 32, 512) == 0
+    stats = (lib.vda_groupnorm_workspace(32, 1369, 256, 32) * 4 + 255) // 256 * 256
+    fused = lib.vda_groupnorm_linear_workspace(32, 1369, 256, 32, 256)
+    assert fused == stats + (256 * 256 * 2 + 256 * 4 + 255) // 256 * 256  # + the folded W' and b'
+    assert lib.vda_groupnorm_linear_workspace(32, 1369, 256, 32, 512) == stats + 32 * 1369 * 256 * 2  # + GN(x)
+    fake = ctypes.c_void_p(0x1000)
+    ws = lib.vda_groupnorm_linear_workspace(2, 100, 256, 32, 256)
+    args = [fake, fake, fake, 2, 100, 256, 32, 1e-6, fake, None, fake, 256, None, fake]
+    assert lib.vda_groupnorm_linear(*args, ws - 16, None) == -22
+    assert b"workspace" in lib.vda_last_error()
+    bad = list(args)
+    bad[5] = 250  # C not a multiple of groups / 8
+    assert lib.vda_groupnorm_linear(*bad, ws, None) == -22
+    bad = list(args)
+    bad[10] = ctypes.c_void_p(0x1008)  # y not 16-byte aligned
+    assert lib.vda_groupnorm_linear(*bad, ws, None) == -22
+    bad = list(args)
+    bad[13] = None  # no workspace
+    assert lib.vda_groupnorm_linear(*bad, ws, None) == -22

@@ -224,6 +224,57 @@ def test_groupnorm(C, S):
     assert rel(y0, ref) < 2e-3
 
 
+@pytest.mark.parametrize("Fr,S,C,N", [(32, 1369, 256, 256), (4, 361, 256, 256), (2, 5476, 256, 256), (3, 12, 256, 256),
+                                      (5, 37, 128, 128), (2, 70, 64, 64), (1, 7, 64, 64), (3, 50, 256, 512),
+                                      (2, 33, 128, 64), (2, 361, 1024, 1024)])
+def test_groupnorm_linear(Fr, S, C, N):
+    """groupnorm_linear (motion_module.py:116-119: GroupNorm(32, eps 1e-6) then proj_in) against torch fp32
+    GroupNorm -> Linear on the same fp16 inputs / weights.  (C, N) with N = C in {64, 128, 256} take the fused
+    kernel (ragged tile tails: S = 12, 7, 37; frames shorter than a 32-row tile), the others the GroupNorm +
+    GEMM composition.  Bar 2e-3 rel-L1: the fused path rounds the normalised operand and gamma (.) W to fp16
+    where the reference rounds GN(x) once, the same order of error as the unfused fp16 path.  One frame
+    carries a large offset (the shifted one-pass variance).  stats_out: per-row (sum, sumsq) of the stored
+    fp16 output, checked against a recomputation from it."""
+    x = rnd(Fr, S, C, seed=140) + 0.3
+    x[Fr // 2] += 20.0
+    g, b = rnd(C, seed=141) * 0.2 + 1, rnd(C, seed=142) * 0.2
+    w, bias = rnd(N, C, scale=C ** -0.5, seed=143), rnd(N, scale=0.1, seed=144)
+    xh = h(x.reshape(-1, C))
+    gn = F.group_norm(xh.float().cpu().view(Fr, S, C).permute(0, 2, 1), 32, g, b, eps=1e-6)
+    ref = gn.permute(0, 2, 1).reshape(-1, C) @ w.t() + bias
+    fused = vda_amd._libvda().vda_groupnorm_linear_fused(C, 32, N) == 1
+    assert fused == (N == C and C in (64, 128, 256))
+    st = torch.full((Fr * S + 1, (N + 255) // 256, 2), float("nan"), device=DEV)
+    y = ops.groupnorm_linear(xh, f32(g), f32(b), Fr, 32, 1e-6, h(w), bias=f32(bias), stats_out=st)
+    assert y.shape == (Fr * S, N) and y.dtype == torch.float16
+    assert rel(y, ref) < 2e-3
+    unf = ops.gemm(ops.groupnorm(xh, f32(g), f32(b), Fr, 32, 1e-6), h(w), bias=f32(bias))
+    assert rel(y, unf) < 2e-3  # and against this library's own two-kernel composition
+    assert torch.equal(y, ops.groupnorm_linear(xh, f32(g), f32(b), Fr, 32, 1e-6, h(w), bias=f32(bias)))  # deterministic
+    yf = y.float().view(Fr * S, -1, min(N, 256))
+    exp = torch.stack([yf.sum(2), (yf * yf).sum(2)], -1)
+    assert torch.allclose(st[:-1], exp, rtol=1e-5, atol=1e-3)
+    assert torch.isnan(st[-1]).all()  # nothing written past row M - 1
+    yn = ops.groupnorm_linear(xh, f32(g), f32(b), Fr, 32, 1e-6, h(w))  # no bias
+    assert rel(yn, ref - bias) < 2e-3
+
+
+def test_groupnorm_linear_large_rows():
+    """The fused kernel at config-5's largest motion-module map (74 x 132 per frame, 32 frames: M = 312,576
+    rows) against the composition."""
+    Fr, S, C = 32, 74 * 132, 256
+    torch.manual_seed(7)
+    xh = (torch.randn(Fr * S, C, device=DEV) * 2 + 0.5).half()
+    g = torch.rand(C, device=DEV) + 0.5
+    b = torch.randn(C, device=DEV) * 0.1
+    w = (torch.randn(C, C, device=DEV) * C ** -0.5).half()
+    bias = torch.randn(C, device=DEV) * 0.1
+    y = ops.groupnorm_linear(xh, g, b, Fr, 32, 1e-6, w, bias=bias)
+    unf = ops.gemm(ops.groupnorm(xh, g, b, Fr, 32, 1e-6), w, bias=bias)
+    assert rel(y, unf) < 2e-3
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1)])
 def test_spatial_attention(B, N, H):
     D = 64

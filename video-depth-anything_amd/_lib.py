@@ -23,6 +23,7 @@ EXPORTED = (
     "vda_version", "vda_epilogue_size", "vda_last_error", "vda_gemm", "vda_conv2d", "vda_conv2d_workspace", "vda_layernorm",
     "vda_conv2d_res2_upsample_ok",
     "vda_row_stats", "vda_groupnorm", "vda_groupnorm_workspace",
+    "vda_groupnorm_linear", "vda_groupnorm_linear_workspace", "vda_groupnorm_linear_fused",
     "vda_spatial_attention", "vda_temporal_attention", "vda_upsample_bilinear", "vda_patch_im2col",
     "vda_depth_head", "vda_depth_head_workspace", "vda_preprocess_frames", "vda_depth_resize",
     "vda_gemm_f32", "vda_conv2d_f32", "vda_layernorm_f32", "vda_groupnorm_f32", "vda_spatial_attention_f32",
@@ -76,6 +77,9 @@ def _declare(lib):
         "vda_row_stats": ([P, L, P, I, I, F, P], I),
         "vda_groupnorm": ([P, P, P, P, I, I, I, I, F, P, P], I),
         "vda_groupnorm_workspace": ([I, I, I, I], L),
+        "vda_groupnorm_linear": ([P, P, P, I, I, I, I, F, P, P, P, I, P, P, L, P], I),
+        "vda_groupnorm_linear_workspace": ([I, I, I, I, I], L),
+        "vda_groupnorm_linear_fused": ([I, I, I], I),
         "vda_spatial_attention": ([P, P, I, I, I, I, F, P], I),
         "vda_temporal_attention": ([P, P, I, I, I, I, I, F, F, P], I),
         "vda_upsample_bilinear": ([P, P, I, I, I, I, I, I, P], I),

@@ -225,10 +225,9 @@ __device__ __forceinline__ void gn_layout(int C, int& cpr, int& rpi) {
   rpi = 256 / cpr;       // rows per block iteration
 }
 
-__global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__ x, float* __restrict__ part, int S, int C,
-                                                         int groups, int nchunk) {
-  __shared__ float red[256 * 16];  // [thread][sum d x8 | sum d^2 x8] (16 KB)
-  const int f = blockIdx.x / nchunk, ch = blockIdx.x % nchunk;
+__device__ __forceinline__ void gn_partial_block(const h16* __restrict__ x, float* __restrict__ part, int S, int C,
+                                                 int groups, int nchunk, int bid, float* red) {
+  const int f = bid / nchunk, ch = bid % nchunk;
   int cpr, rpi;
   gn_layout(C, cpr, rpi);
   const int tid = threadIdx.x;
@@ -275,6 +274,48 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__
     for (int j = 0; j < 8; ++j) { out[2 * j] = a1[j]; out[2 * j + 1] = a2[j]; }
   }
 }
+
+__global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__ x, float* __restrict__ part, int S, int C,
+                                                         int groups, int nchunk) {
+  __shared__ float red[256 * 16];  // [thread][sum d x8 | sum d^2 x8] (16 KB)
+  gn_partial_block(x, part, S, C, groups, nchunk, blockIdx.x, red);
+}
+
+// groupnorm_linear's first launch: blocks [0, F * nchunk) are gn_partial; the K / 16 (or K / 32) after them
+// fold the GroupNorm affine into the weights once per call, W' = fp16(W gamma) ([N, K] half, plain rows)
+// and b' = W beta + b (fp32, the TPR lanes of a row summed by shuffles in a fixed order).
+template <int K>
+__global__ __launch_bounds__(256) void gnl_prep_kernel(const h16* __restrict__ x, float* __restrict__ part, int S,
+                                                       int C, int groups, int nchunk, int npartial, const h16* __restrict__ w,
+                                                       const float* __restrict__ gam, const float* __restrict__ bet,
+                                                       const float* __restrict__ bias, h16* __restrict__ wf,
+                                                       float* __restrict__ bf) {
+  __shared__ float red[256 * 16];
+  if ((int)blockIdx.x < npartial) {
+    gn_partial_block(x, part, S, C, groups, nchunk, blockIdx.x, red);  // C == K, runtime as in gn_partial_kernel
+    return;
+  }
+  constexpr int CH = K / 8, TPR = CH < 16 ? CH : 16, RPB = 256 / TPR, CPT = CH / TPR;
+  const int tid = threadIdx.x, n = ((int)blockIdx.x - npartial) * RPB + tid / TPR, l = tid % TPR;
+  float d = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = l * CPT + k;
+    const h8 v = __builtin_bit_cast(h8, ldg16(w + (long)n * K + c * 8));
+    h8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      o[j] = (h16)((float)v[j] * gam[c * 8 + j]);
+      d = fmaf((float)v[j], bet[c * 8 + j], d);
+    }
+    stg16(wf + (long)n * K + c * 8, __builtin_bit_cast(uint4, o));
+  }
+#pragma unroll
+  for (int off = TPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
+  if (l == 0) bf[n] = d + (bias ? bias[n] : 0.f);
+}
+template <int K>
+constexpr int gnl_fold_blocks() { return K * (K / 8 < 16 ? K / 8 : 16) / 256; }
 
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const h16* __restrict__ x, const float* __restrict__ part,
                                                          float* __restrict__ stats, int S, int C, int groups, int nchunk,
@@ -329,6 +370,143 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = (h16)fmaf((float)v[j], sc[j], of[j]);
     stg16(y + fo + (long)r * C + cc * 8, __builtin_bit_cast(uint4, o));
+  }
+}
+
+// GroupNorm -> Linear (motion_module.py:116-119: norm, rearrange, proj_in), the GroupNorm applied to
+// the GEMM's operand in registers instead of through a normalised copy of x in HBM.
+//   GN(x) W^T + b = ((x - mean_fg) rstd_fg) (W diag(gamma))^T + (W beta + b)
+// so the block stages W' = fp16(W * gamma[k]) in LDS once (128 KiB at C = 256: one block per CU) with
+// b' = W beta + b, and each of its 8 waves streams 16-row tiles of x: z = fp16(fma(x, rstd, -mean rstd))
+// per element, z W'^T on v_mfma_f32_16x16x32_f16 (A = W' fragments from LDS, B = z), + b', fp16 store
+// and, optionally, the per-row (sum, sum of squares) of the stored row for a following LN-folded GEMM.
+// K = N = C in {64, 128, 256}, 32 groups (C / 32 channels each).  At k-step s lane group q takes the
+// 16-byte chunk 4s + q of its row (one load instruction: 64 contiguous bytes of each of 16 rows).  A wave
+// issues all loads of its next tile (x and the rows' group statistics) before it computes the current
+// one: two waves per SIMD, 8 KiB of x in flight per wave.  The transform is v_fma_mix_f32 on the packed
+// fp16 pairs: the SLP-packed form hipcc chose by itself (v_pk_fma_f32 broadcasting rstd through op_sel)
+// gave wrong values on lanes 48-63 for some k-steps on gfx950 (tools/dbg_gnl2.py).
+// Roofline: HBM (x in, y out: 4 C bytes per row); the W' fragment reads (C^2 / 8 bytes of LDS per 16-row
+// tile) and the MFMAs stay under it.
+constexpr int GNL_GROUPS = 32;
+constexpr int GNL_WAVES = 8;
+
+template <int K>
+__global__ __launch_bounds__(64 * GNL_WAVES, 1) void gn_linear_kernel(
+    const h16* __restrict__ x, const float* __restrict__ stats, const h16* __restrict__ wf,
+    const float* __restrict__ bf, h16* __restrict__ y, float* __restrict__ stats_out, int M, int S, int ntiles) {
+  constexpr int N = K;
+  constexpr int NTH = 64 * GNL_WAVES;
+  constexpr int CH = K / 8;                      // 16-byte chunks per row
+  constexpr int KS = K / 32;                     // MFMA k-steps; step s, lane group q: chunk 4s + q
+  constexpr int NT = N / 16;                     // 16-column tiles of the output
+  constexpr int SWZ = (CH >= 16 ? 16 : CH) - 1;  // chunk XOR of the W' rows: 16 lanes, 16 distinct slots
+  constexpr int CG = K / GNL_GROUPS;             // channels per group
+  constexpr int GPC = 8 / CG;                    // groups per chunk
+  __shared__ __attribute__((aligned(16))) h16 sw[N * K];
+  __shared__ __attribute__((aligned(16))) float sb[N];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  {  // W' (folded by gnl_prep_kernel) into LDS with the chunk XOR, every load in flight at once
+    constexpr int R = N * CH / NTH;
+    static_assert(N * CH % NTH == 0, "whole staging rounds");
+    uint4 wv[R];
+#pragma unroll
+    for (int it = 0; it < R; ++it) wv[it] = ldg16(wf + (long)(tid + it * NTH) * 8);
+#pragma unroll
+    for (int it = 0; it < R; ++it) {
+      const int i = tid + it * NTH, n = i / CH, c = i - n * CH;
+      *reinterpret_cast<uint4*>(&sw[n * K + ((c ^ (n & SWZ)) * 8)]) = wv[it];
+    }
+    if (tid < N) sb[tid] = bf[tid];
+  }
+  __syncthreads();
+
+  const int q = lane >> 4, r16 = lane & 15;
+  const int tstride = gridDim.x * GNL_WAVES;
+  int t = blockIdx.x * GNL_WAVES + wave;
+  if (t >= ntiles) return;  // no barrier below this point
+  const float2* st2 = reinterpret_cast<const float2*>(stats);
+  auto load = [&](int tt, uint4 (&xb)[KS], float2 (&sv)[KS][GPC]) {
+    const int m = min(tt * 16 + r16, M - 1);
+    const h16* xp = x + (long)m * K + q * 8;
+    const float2* sp = st2 + (long)(m / S) * GNL_GROUPS + q * GPC;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) xb[s] = ldg16(xp + s * 32);
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+#pragma unroll
+      for (int k = 0; k < GPC; ++k) sv[s][k] = sp[4 * s * GPC + k];
+  };
+  const h16* wq = sw + r16 * K;
+  auto compute = [&](int tt, const uint4 (&xb)[KS], const float2 (&sv)[KS][GPC]) {
+    f4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      float rs[GPC], nm[GPC];
+#pragma unroll
+      for (int k = 0; k < GPC; ++k) {
+        rs[k] = sv[s][k].y;
+        nm[k] = -sv[s][k].x * sv[s][k].y;
+      }
+      const unsigned xv[4] = {xb[s].x, xb[s].y, xb[s].z, xb[s].w};
+      unsigned zv[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {  // v_fma_mix_f32 on the packed fp16 pairs, one rounding to fp16
+        const float lo = fma_mix_lo(rs[(2 * p) / CG], xv[p], nm[(2 * p) / CG]);
+        const float hi = fma_mix_hi(rs[(2 * p + 1) / CG], xv[p], nm[(2 * p + 1) / CG]);
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        zv[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{lo, hi}, h2));
+      }
+      const h8 z = __builtin_bit_cast(h8, make_uint4(zv[0], zv[1], zv[2], zv[3]));
+      const int cs = ((4 * s + q) ^ (r16 & SWZ)) * 8;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = mfma16(*reinterpret_cast<const h8*>(wq + j * 16 * K + cs), z, acc[j]);
+    }
+    // epilogue: lane holds y[m = 16 tt + r16][n = 16j + 4q + i]
+    const int m = tt * 16 + r16;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float4 b = *reinterpret_cast<const float4*>(&sb[j * 16 + 4 * q]);
+      h4 o;
+      o[0] = (h16)(acc[j][0] + b.x);
+      o[1] = (h16)(acc[j][1] + b.y);
+      o[2] = (h16)(acc[j][2] + b.z);
+      o[3] = (h16)(acc[j][3] + b.w);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float f = (float)o[i];
+        s1 += f;
+        s2 = fmaf(f, f, s2);
+      }
+      if (m < M) *reinterpret_cast<h4*>(y + (long)m * N + j * 16 + 4 * q) = o;
+    }
+    if (stats_out) {  // sum over the 4 lane groups (lane bits 4, 5), then one (sum, sumsq) per row
+      float a, b;
+      swap16_pair(s1, a, b);
+      s1 = half_sum(a + b);
+      swap16_pair(s2, a, b);
+      s2 = half_sum(a + b);
+      if (q == 0 && m < M) *reinterpret_cast<float2*>(stats_out + 2L * m) = make_float2(s1, s2);
+    }
+  };
+  // two register sets, the next tile's loads issued before the current tile's MFMAs; a wave past the
+  // end re-reads its own tile (no branch around the loads) and exits after its last store
+  uint4 xa[KS], xb[KS];
+  float2 sa[KS][GPC], sb2[KS][GPC];
+  load(t, xa, sa);
+  while (true) {
+    const int t1 = t + tstride;
+    load(t1 < ntiles ? t1 : t, xb, sb2);
+    compute(t, xa, sa);
+    if (t1 >= ntiles) break;
+    const int t2 = t1 + tstride;
+    load(t2 < ntiles ? t2 : t1, xa, sa);
+    compute(t1, xb, sb2);
+    if (t2 >= ntiles) break;
+    t = t2;
   }
 }
 
@@ -415,6 +593,77 @@ extern "C" int vda_groupnorm(const void* x, void* y, const float* gamma, const f
     hipLaunchKernelGGL(groupnorm_kernel<4>, grid, dim3(256), 0, st, (const h16*)x, (h16*)y, gamma, beta, S, C, groups, eps);
   else
     hipLaunchKernelGGL(groupnorm_kernel<2>, grid, dim3(256), 0, st, (const h16*)x, (h16*)y, gamma, beta, S, C, groups, eps);
+  VDA_LAUNCH_CHECK();
+  return 0;
+}
+
+// ---- GroupNorm -> Linear ------------------------------------------------------------------------
+namespace {
+bool gnl_fused(int32_t C, int32_t groups, int32_t N) {
+  return groups == GNL_GROUPS && N == C && (C == 64 || C == 128 || C == 256);
+}
+int64_t gnl_stats_bytes(int32_t F, int32_t S, int32_t C, int32_t groups) {
+  return (vda_groupnorm_workspace(F, S, C, groups) * 4 + 255) / 256 * 256;
+}
+// fused route: [GroupNorm partials + (mean, rstd)] [W' half N x C] [b' float N]
+int64_t gnl_fold_bytes(int32_t C, int32_t N) { return ((int64_t)N * C * 2 + (int64_t)N * 4 + 255) / 256 * 256; }
+}  // namespace
+
+extern "C" int vda_groupnorm_linear_fused(int32_t C, int32_t groups, int32_t N) { return gnl_fused(C, groups, N) ? 1 : 0; }
+
+extern "C" int64_t vda_groupnorm_linear_workspace(int32_t F, int32_t S, int32_t C, int32_t groups, int32_t N) {
+  if (F <= 0 || S <= 0 || C <= 0 || groups <= 0 || N <= 0) return 0;
+  const int64_t b = gnl_stats_bytes(F, S, C, groups);
+  return gnl_fused(C, groups, N) ? b + gnl_fold_bytes(C, N)
+                                 : b + (int64_t)F * S * C * 2;  // the normalised copy of x (unfused route)
+}
+
+extern "C" int vda_groupnorm_linear(const void* x, const float* gamma, const float* beta, int32_t F, int32_t S,
+                                    int32_t C, int32_t groups, float eps, const void* w, const float* bias, void* y,
+                                    int32_t N, float* stats_out, void* ws, int64_t ws_bytes, void* stream) {
+  VDA_CHECK_ARG(x && gamma && beta && w && y && ws, "null pointer");
+  VDA_CHECK_ARG(F > 0 && S > 0 && groups > 0 && C % groups == 0 && C % 8 == 0 && C <= 2048 && N > 0,
+                "C must be a multiple of 8 and of groups, <= 2048");
+  VDA_CHECK_ARG((long)F * S <= 0x7fffffffL, "F * S rows must fit int32");
+  VDA_CHECK_ARG(ws_bytes >= vda_groupnorm_linear_workspace(F, S, C, groups, N), "workspace too small");
+  VDA_CHECK_ARG((uintptr_t)ws % 16 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)w % 16 == 0 && (uintptr_t)y % 16 == 0,
+                "x, w, y and ws must be 16-byte aligned");
+  hipStream_t st = (hipStream_t)stream;
+  const int M = F * S;
+  float* wsf = (float*)ws;
+  if (!gnl_fused(C, groups, N)) {  // the two-kernel composition: vda_groupnorm into ws, then vda_gemm
+    void* xn = (char*)ws + gnl_stats_bytes(F, S, C, groups);
+    int rc = vda_groupnorm(x, xn, gamma, beta, F, S, C, groups, eps, wsf, stream);
+    if (rc) return rc;
+    vda_epilogue e = {};
+    e.bias = bias;
+    e.rdiv = e.rmod = 1;
+    e.stats_out = stats_out;
+    return vda_gemm(xn, C, w, y, N, M, N, C, &e, stream);
+  }
+  const int nchunk = (S + gn_rows(C) - 1) / gn_rows(C);
+  float* stats = wsf + 2L * F * nchunk * C;
+  h16* wf = (h16*)((char*)ws + gnl_stats_bytes(F, S, C, groups));
+  float* bf = (float*)(wf + (long)N * C);
+  const int npart = F * nchunk;
+  const int ntiles = (M + 15) / 16;
+  const int nblk = std::min(vda_cu_count(), (ntiles + GNL_WAVES - 1) / GNL_WAVES);
+#define VDA_GNL(KK)                                                                                                  \
+  do {                                                                                                               \
+    hipLaunchKernelGGL(gnl_prep_kernel<KK>, dim3(npart + gnl_fold_blocks<KK>()), dim3(256), 0, st, (const h16*)x, wsf, \
+                       S, C, groups, nchunk, npart, (const h16*)w, gamma, beta, bias, wf, bf);                           \
+    hipLaunchKernelGGL(gn_finalize_kernel, dim3(F * groups), dim3(64), 0, st, (const h16*)x, (const float*)wsf, stats, \
+                       S, C, groups, nchunk, eps);                                                                   \
+    hipLaunchKernelGGL(gn_linear_kernel<KK>, dim3(nblk), dim3(64 * GNL_WAVES), 0, st, (const h16*)x,                  \
+                       (const float*)stats, (const h16*)wf, (const float*)bf, (h16*)y, stats_out, M, S, ntiles);     \
+  } while (0)
+  if (C == 256)
+    VDA_GNL(256);
+  else if (C == 128)
+    VDA_GNL(128);
+  else
+    VDA_GNL(64);
+#undef VDA_GNL
   VDA_LAUNCH_CHECK();
   return 0;
 }

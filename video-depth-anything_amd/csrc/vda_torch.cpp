@@ -315,6 +315,52 @@ Tensor groupnorm(const Tensor& x, const Tensor& gamma, const Tensor& beta, int64
   return out;
 }
 
+// GroupNorm -> Linear (motion_module.py:116-119): fp16 through vda_groupnorm_linear (fused where
+// vda_groupnorm_linear_fused says so), fp32 mode as vda_groupnorm_f32 + vda_gemm_f32.
+Tensor groupnorm_linear(const Tensor& x, const Tensor& gamma, const Tensor& beta, int64_t frames, int64_t groups,
+                        double eps, const Tensor& w, OptT bias, OptT stats_out) {
+  const auto dt = act_dtype(x);
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "vda groupnorm_linear: x must be a contiguous [F*S, C] matrix");
+  TORCH_CHECK(frames > 0 && x.size(0) % frames == 0, "vda groupnorm_linear: rows must be a multiple of frames");
+  TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(1), "vda groupnorm_linear: w must be [N, C], got ", w.sizes());
+  const int64_t M = x.size(0), C = x.size(1), N = w.size(0), S = M / frames;
+  if (stats_out)
+    TORCH_CHECK(dt == at::kHalf && stats_out->dim() == 3 && stats_out->size(0) >= M &&
+                    stats_out->size(1) == (N + 255) / 256 && stats_out->size(2) == 2 &&
+                    stats_out->scalar_type() == at::kFloat && stats_out->is_contiguous(),
+                "vda groupnorm_linear: stats_out must be a contiguous float [M, ceil(N / 256), 2] (fp16 mode)");
+  Tensor out = at::empty({M, N}, x.options());
+  if (x.is_meta()) return out;
+  const at::OptionalDeviceGuard g(x.device());
+  need_contig(gamma, at::kFloat, "gamma", x);
+  need_contig(beta, at::kFloat, "beta", x);
+  need_contig(w, dt, "w", x);
+  if (bias) need_contig(*bias, at::kFloat, "bias", x);
+  if (stats_out) need_contig(*stats_out, at::kFloat, "stats_out", x);
+  if (dt == at::kFloat) {
+    Tensor xn = at::empty_like(x);
+    check_rc(vda_groupnorm_f32((const float*)x.data_ptr(), (float*)xn.data_ptr(), (const float*)gamma.data_ptr(),
+                               (const float*)beta.data_ptr(), frames, S, C, groups, (float)eps, stream_of(x)),
+             "vda_groupnorm_f32");
+    vda_epilogue e;
+    std::memset(&e, 0, sizeof(e));
+    e.bias = (const float*)ptr(bias);
+    e.rdiv = e.rmod = 1;
+    check_rc(vda_gemm_f32((const float*)xn.data_ptr(), C, (const float*)w.data_ptr(), (float*)out.data_ptr(), N,
+                          (int32_t)M, (int32_t)N, (int32_t)C, &e, stream_of(x)),
+             "vda_gemm_f32");
+    return out;
+  }
+  const int64_t wsb = vda_groupnorm_linear_workspace(frames, S, C, groups, N);
+  Tensor ws = at::empty({std::max<int64_t>(wsb, 16)}, x.options().dtype(at::kByte));
+  check_rc(vda_groupnorm_linear(x.data_ptr(), (const float*)gamma.data_ptr(), (const float*)beta.data_ptr(), frames,
+                                S, C, groups, (float)eps, w.data_ptr(), (const float*)ptr(bias), out.data_ptr(), N,
+                                stats_out ? (float*)stats_out->data_ptr() : nullptr, ws.data_ptr(), wsb,
+                                stream_of(x)),
+           "vda_groupnorm_linear");
+  return out;
+}
+
 // ---- attention ---------------------------------------------------------------------------------
 Tensor spatial_attention(const Tensor& qkv, int64_t B, int64_t N, int64_t H, int64_t D) {
   const auto dt = act_dtype(qkv);
@@ -465,6 +511,8 @@ TORCH_LIBRARY(vda, m) {
         "int act=0, Tensor? res=None, Tensor? res2=None, int[]? up=None) -> Tensor");
   m.def("layernorm(Tensor x, Tensor gamma, Tensor beta, float eps, int skip_period=0, int? rows=None) -> Tensor");
   m.def("groupnorm(Tensor x, Tensor gamma, Tensor beta, int frames, int groups, float eps) -> Tensor");
+  m.def("groupnorm_linear(Tensor x, Tensor gamma, Tensor beta, int frames, int groups, float eps, Tensor w, "
+        "Tensor? bias=None, Tensor(b!)? stats_out=None) -> Tensor");
   m.def("spatial_attention(Tensor qkv, int B, int N, int H, int D=64) -> Tensor");
   m.def("temporal_attention(Tensor qkv, int B, int T, int S, int H, int D, float rope_theta=0.) -> Tensor");
   m.def("upsample_bilinear(Tensor x, int Ho, int Wo) -> Tensor");
@@ -483,6 +531,7 @@ TORCH_LIBRARY(vda, m) {
     m.impl("layernorm", &layernorm);                          \
     m.impl("row_stats", &row_stats);                          \
     m.impl("groupnorm", &groupnorm);                          \
+    m.impl("groupnorm_linear", &groupnorm_linear);            \
     m.impl("spatial_attention", &spatial_attention);          \
     m.impl("temporal_attention", &temporal_attention);        \
     m.impl("upsample_bilinear", &upsample_bilinear);          \

@@ -238,7 +238,9 @@ class VideoDepthAnything(nn.Module):
     qkv / fc1 GEMMs and the motion modules' attention-block LayerNorms into their q/k/v GEMMs (fp16
     mode), ``epilogue_stats`` takes those LayerNorms' row statistics from the
     proj / fc2 epilogues instead of a separate pass, ``fold_ff_norm`` folds the motion modules' ff_norm into
-    their GEGLU GEMM (fp16 mode, with ``fold_layernorms``), ``dynamic_tiles`` lets the encoder's persistent GEMMs
+    their GEGLU GEMM (fp16 mode, with ``fold_layernorms``), ``fuse_groupnorm_linear`` runs each motion
+    module's GroupNorm + proj_in as the one ``groupnorm_linear`` op (the normalised input never written),
+    ``dynamic_tiles`` lets the encoder's persistent GEMMs
     take their tiles by atomic ticket (per-stream counters, ``ops.sched_counters``) instead of a fixed
     stride.  No environment variable changes the schedule."""
 
@@ -246,6 +248,7 @@ class VideoDepthAnything(nn.Module):
     epilogue_stats: bool = True
     dynamic_tiles: bool = False
     fold_ff_norm: bool = False  # built and tested; same-box forward A/B 693.7 -> 690.0 frames/s (r06_ab_ffold.log)
+    fuse_groupnorm_linear: bool = True
 
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
@@ -481,11 +484,15 @@ class VideoDepthAnything(nn.Module):
         per-row partial sums."""
         C = q.C
         M = x.shape[0]
-        xn = ops.groupnorm(x, q.gnw, q.gnb, B * T, 32, 1e-6)
         fold = [a.fold and S >= 256 and M >= 4096 for a in q.attn]
         fffold = q.fffold and bool(self.fold_ff_norm)
         st = torch.empty(M + 1, (C + 255) // 256, 2, device=x.device) if any(fold) or fffold else None
-        h = ops.gemm(xn, q.pin_w, bias=q.pin_b, stats_out=st if fold[0] else None)
+        if self.fuse_groupnorm_linear:  # norm + proj_in as one op (motion_module.py:116-119)
+            h = ops.groupnorm_linear(x, q.gnw, q.gnb, B * T, 32, 1e-6, q.pin_w, bias=q.pin_b,
+                                     stats_out=st if fold[0] else None)
+        else:
+            xn = ops.groupnorm(x, q.gnw, q.gnb, B * T, 32, 1e-6)
+            h = ops.gemm(xn, q.pin_w, bias=q.pin_b, stats_out=st if fold[0] else None)
         for i, a in enumerate(q.attn):
             if fold[i]:  # rstd (h W'^T - mean colsum) + W beta + pe[t] W^T
                 qkv = ops.gemm(h, a.qkv_wg, bias=a.qkv_bb, rowbias=a.pe_bias, rdiv=S, rmod=T, ln_stats=st,

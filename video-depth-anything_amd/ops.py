@@ -136,6 +136,16 @@ def groupnorm(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, 
     return _vda().groupnorm(x, gamma, beta, int(frames), int(groups), float(eps))
 
 
+def groupnorm_linear(x: Tensor, gamma: Tensor, beta: Tensor, frames: int, groups: int, eps: float, w: Tensor, *,
+                     bias=None, stats_out=None) -> Tensor:
+    """GroupNorm on NHWC frames then Linear: x [F*S, C] -> GN(x) @ w[N, C]^T + bias, [F*S, N]
+    (motion_module.py:116-119, norm + proj_in).  fp16: one fused kernel for groups 32, N = C in
+    {64, 128, 256} (vda.h vda_groupnorm_linear), else GroupNorm + GEMM through a workspace; ``stats_out``
+    ([F*S, 1, 2] fp32) receives the per-row (sum, sumsq) of the output for a following LN-folded GEMM."""
+    _need(x, x.dtype, "x")
+    return _vda().groupnorm_linear(x, gamma, beta, int(frames), int(groups), float(eps), w, bias, stats_out)
+
+
 def spatial_attention(qkv: Tensor, B: int, N: int, H: int, D: int = 64) -> Tensor:
     _need(qkv, qkv.dtype, "qkv")
     return _vda().spatial_attention(qkv, int(B), int(N), int(H), int(D))
