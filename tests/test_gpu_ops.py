@@ -231,8 +231,9 @@ def test_groupnorm_linear(Fr, S, C, N):
     """groupnorm_linear (motion_module.py:116-119: GroupNorm(32, eps 1e-6) then proj_in) against torch fp32
     GroupNorm -> Linear on the same fp16 inputs / weights.  (C, N) with N = C in {64, 128, 256} take the fused
     kernel (ragged tile tails: S = 12, 7, 37; frames shorter than a 32-row tile), the others the GroupNorm +
-    GEMM composition.  Bar 2e-3 rel-L1: the fused path rounds the normalised operand and gamma (.) W to fp16
-    where the reference rounds GN(x) once, the same order of error as the unfused fp16 path.  One frame
+    GEMM composition.  Bar 2e-3 rel-L1 (fp16 output rounding and the fp16 normalised operand, as the reference's
+    autocast GroupNorm -> Linear); against this library's composition 2e-4: the fused kernel forms gn_apply's
+    operand bits and differs only in the fp32 accumulation order.  One frame
     carries a large offset (the shifted one-pass variance).  stats_out: per-row (sum, sumsq) of the stored
     fp16 output, checked against a recomputation from it."""
     x = rnd(Fr, S, C, seed=140) + 0.3
@@ -249,7 +250,7 @@ def test_groupnorm_linear(Fr, S, C, N):
     assert y.shape == (Fr * S, N) and y.dtype == torch.float16
     assert rel(y, ref) < 2e-3
     unf = ops.gemm(ops.groupnorm(xh, f32(g), f32(b), Fr, 32, 1e-6), h(w), bias=f32(bias))
-    assert rel(y, unf) < 2e-3  # and against this library's own two-kernel composition
+    assert rel(y, unf) < 2e-4  # and against this library's own two-kernel composition
     assert torch.equal(y, ops.groupnorm_linear(xh, f32(g), f32(b), Fr, 32, 1e-6, h(w), bias=f32(bias)))  # deterministic
     yf = y.float().view(Fr * S, -1, min(N, 256))
     exp = torch.stack([yf.sum(2), (yf * yf).sum(2)], -1)
@@ -261,7 +262,7 @@ def test_groupnorm_linear(Fr, S, C, N):
 
 def test_groupnorm_linear_large_rows():
     """The fused kernel at config-5's largest motion-module map (74 x 132 per frame, 32 frames: M = 312,576
-    rows) against the composition."""
+    rows) against the GroupNorm + GEMM composition (round 6: bit-identical, tools/ab_gnl.py)."""
     Fr, S, C = 32, 74 * 132, 256
     torch.manual_seed(7)
     xh = (torch.randn(Fr * S, C, device=DEV) * 2 + 0.5).half()
@@ -271,8 +272,8 @@ def test_groupnorm_linear_large_rows():
     bias = torch.randn(C, device=DEV) * 0.1
     y = ops.groupnorm_linear(xh, g, b, Fr, 32, 1e-6, w, bias=bias)
     unf = ops.gemm(ops.groupnorm(xh, g, b, Fr, 32, 1e-6), w, bias=bias)
-    assert rel(y, unf) < 2e-3
-    torch.cuda.synchronize()
+    # the same operand bits (gn_apply's fma) and, against the phased GEMM, the same K order: bit-identical
+    assert torch.equal(y, unf)
 
 
 @pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1)])

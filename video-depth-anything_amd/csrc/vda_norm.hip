@@ -281,41 +281,6 @@ __global__ __launch_bounds__(256) void gn_partial_kernel(const h16* __restrict__
   gn_partial_block(x, part, S, C, groups, nchunk, blockIdx.x, red);
 }
 
-// groupnorm_linear's first launch: blocks [0, F * nchunk) are gn_partial; the K / 16 (or K / 32) after them
-// fold the GroupNorm affine into the weights once per call, W' = fp16(W gamma) ([N, K] half, plain rows)
-// and b' = W beta + b (fp32, the TPR lanes of a row summed by shuffles in a fixed order).
-template <int K>
-__global__ __launch_bounds__(256) void gnl_prep_kernel(const h16* __restrict__ x, float* __restrict__ part, int S,
-                                                       int C, int groups, int nchunk, int npartial, const h16* __restrict__ w,
-                                                       const float* __restrict__ gam, const float* __restrict__ bet,
-                                                       const float* __restrict__ bias, h16* __restrict__ wf,
-                                                       float* __restrict__ bf) {
-  __shared__ float red[256 * 16];
-  if ((int)blockIdx.x < npartial) {
-    gn_partial_block(x, part, S, C, groups, nchunk, blockIdx.x, red);  // C == K, runtime as in gn_partial_kernel
-    return;
-  }
-  constexpr int CH = K / 8, TPR = CH < 16 ? CH : 16, RPB = 256 / TPR, CPT = CH / TPR;
-  const int tid = threadIdx.x, n = ((int)blockIdx.x - npartial) * RPB + tid / TPR, l = tid % TPR;
-  float d = 0.f;
-#pragma unroll
-  for (int k = 0; k < CPT; ++k) {
-    const int c = l * CPT + k;
-    const h8 v = __builtin_bit_cast(h8, ldg16(w + (long)n * K + c * 8));
-    h8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      o[j] = (h16)((float)v[j] * gam[c * 8 + j]);
-      d = fmaf((float)v[j], bet[c * 8 + j], d);
-    }
-    stg16(wf + (long)n * K + c * 8, __builtin_bit_cast(uint4, o));
-  }
-#pragma unroll
-  for (int off = TPR / 2; off > 0; off >>= 1) d += __shfl_xor(d, off, 64);
-  if (l == 0) bf[n] = d + (bias ? bias[n] : 0.f);
-}
-template <int K>
-constexpr int gnl_fold_blocks() { return K * (K / 8 < 16 ? K / 8 : 16) / 256; }
 
 __global__ __launch_bounds__(64) void gn_finalize_kernel(const h16* __restrict__ x, const float* __restrict__ part,
                                                          float* __restrict__ stats, int S, int C, int groups, int nchunk,
@@ -359,7 +324,7 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x
     const int c = cc * 8 + j, g = c / cg;
     const float mean = stats[(f * groups + g) * 2], rstd = stats[(f * groups + g) * 2 + 1];
     sc[j] = rstd * gam[c];
-    of[j] = bet[c] - mean * sc[j];
+    of[j] = __builtin_fmaf(-mean, sc[j], bet[c]);  // spelled out: gn_linear_kernel forms the same bits
   }
   const long fo = (long)f * S * C;
   const int rend = min(S, (ch + 1) * gn_rows(C));
@@ -373,51 +338,60 @@ __global__ __launch_bounds__(256) void gn_apply_kernel(const h16* __restrict__ x
   }
 }
 
-// GroupNorm -> Linear (motion_module.py:116-119: norm, rearrange, proj_in), the GroupNorm applied to
-// the GEMM's operand in registers instead of through a normalised copy of x in HBM.
-//   GN(x) W^T + b = ((x - mean_fg) rstd_fg) (W diag(gamma))^T + (W beta + b)
-// so the block stages W' = fp16(W * gamma[k]) in LDS once (128 KiB at C = 256: one block per CU) with
-// b' = W beta + b, and each of its 8 waves streams 16-row tiles of x: z = fp16(fma(x, rstd, -mean rstd))
-// per element, z W'^T on v_mfma_f32_16x16x32_f16 (A = W' fragments from LDS, B = z), + b', fp16 store
-// and, optionally, the per-row (sum, sum of squares) of the stored row for a following LN-folded GEMM.
-// K = N = C in {64, 128, 256}, 32 groups (C / 32 channels each).  At k-step s lane group q takes the
-// 16-byte chunk 4s + q of its row (one load instruction: 64 contiguous bytes of each of 16 rows).  A wave
-// issues all loads of its next tile (x and the rows' group statistics) before it computes the current
-// one: two waves per SIMD, 8 KiB of x in flight per wave.  The transform is v_fma_mix_f32 on the packed
-// fp16 pairs: the SLP-packed form hipcc chose by itself (v_pk_fma_f32 broadcasting rstd through op_sel)
-// gave wrong values on lanes 48-63 for some k-steps on gfx950 (tools/dbg_gnl2.py).
-// Roofline: HBM (x in, y out: 4 C bytes per row); the W' fragment reads (C^2 / 8 bytes of LDS per 16-row
+// GroupNorm -> Linear (motion_module.py:116-119: norm, rearrange, proj_in) with the normalisation applied
+// to the GEMM operand in registers instead of through a normalised copy of x in HBM.  The operand is
+// exactly gn_apply's output, z = fp16(fma(x, sc, of)), sc = rstd_fg gamma_c, of = fma(-mean_fg, sc, beta_c),
+// so the fused route and the GroupNorm + GEMM composition differ only in the fp32 accumulation order.
+// A block (8 waves, one per CU: the weights are resident) stages W [N, K] into LDS once (128 KiB at
+// C = 256, 16-B chunks XOR-swizzled by row) with gamma, beta and the bias; each wave streams 16-row
+// tiles: per k-step s, lane group q takes the 16-byte chunk 4s + q of its row (one load instruction =
+// 64 contiguous bytes of 16 rows), forms z with v_fma_mix_f32 on the packed fp16 pairs, and runs
+// v_mfma_f32_16x16x32_f16 with A = W fragments from LDS, B = z; + bias, fp16 8-B stores, optional per-row
+// (sum, sum of squares) for a following LN-folded GEMM.  The next tile's x and per-row group statistics
+// are loaded before the current tile's MFMAs (two register sets, two waves per SIMD).  Each lane looks up
+// its own row's frame, so tiles may span frames (any S).  K = N = C in {64, 128, 256}, 32 groups.
+// hipcc's own SLP packing of this transform (v_pk_fma_f32 broadcasting the scale through op_sel) gave
+// wrong values on lanes 48-63 for some k-steps on gfx950 (tools/dbg_gnl2.py): the
+// v_fma_mix form is spelled out.
+// Roofline: HBM (x in, y out: 4 C bytes per row); the W fragment reads (C^2 / 8 bytes of LDS per 16-row
 // tile) and the MFMAs stay under it.
 constexpr int GNL_GROUPS = 32;
 constexpr int GNL_WAVES = 8;
 
 template <int K>
 __global__ __launch_bounds__(64 * GNL_WAVES, 1) void gn_linear_kernel(
-    const h16* __restrict__ x, const float* __restrict__ stats, const h16* __restrict__ wf,
-    const float* __restrict__ bf, h16* __restrict__ y, float* __restrict__ stats_out, int M, int S, int ntiles) {
+    const h16* __restrict__ x, const float* __restrict__ stats, const h16* __restrict__ w,
+    const float* __restrict__ gam, const float* __restrict__ bet, const float* __restrict__ bias,
+    h16* __restrict__ y, float* __restrict__ stats_out, int M, int S, int ntiles) {
   constexpr int N = K;
   constexpr int NTH = 64 * GNL_WAVES;
   constexpr int CH = K / 8;                      // 16-byte chunks per row
   constexpr int KS = K / 32;                     // MFMA k-steps; step s, lane group q: chunk 4s + q
   constexpr int NT = N / 16;                     // 16-column tiles of the output
-  constexpr int SWZ = (CH >= 16 ? 16 : CH) - 1;  // chunk XOR of the W' rows: 16 lanes, 16 distinct slots
+  constexpr int SWZ = (CH >= 16 ? 16 : CH) - 1;  // chunk XOR of the W rows: 16 lanes, 16 distinct slots
   constexpr int CG = K / GNL_GROUPS;             // channels per group
   constexpr int GPC = 8 / CG;                    // groups per chunk
   __shared__ __attribute__((aligned(16))) h16 sw[N * K];
   __shared__ __attribute__((aligned(16))) float sb[N];
+  __shared__ __attribute__((aligned(16))) float sg[K];
+  __shared__ __attribute__((aligned(16))) float sbe[K];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  {  // W' (folded by gnl_prep_kernel) into LDS with the chunk XOR, every load in flight at once
+  {  // W into LDS with the chunk XOR, every load in flight at once; gamma / beta / bias beside it
     constexpr int R = N * CH / NTH;
     static_assert(N * CH % NTH == 0, "whole staging rounds");
     uint4 wv[R];
 #pragma unroll
-    for (int it = 0; it < R; ++it) wv[it] = ldg16(wf + (long)(tid + it * NTH) * 8);
+    for (int it = 0; it < R; ++it) wv[it] = ldg16(w + (long)(tid + it * NTH) * 8);
 #pragma unroll
     for (int it = 0; it < R; ++it) {
       const int i = tid + it * NTH, n = i / CH, c = i - n * CH;
       *reinterpret_cast<uint4*>(&sw[n * K + ((c ^ (n & SWZ)) * 8)]) = wv[it];
     }
-    if (tid < N) sb[tid] = bf[tid];
+    if (tid < N) sb[tid] = bias ? bias[tid] : 0.f;
+    if (tid < K) {
+      sg[tid] = gam[tid];
+      sbe[tid] = bet[tid];
+    }
   }
   __syncthreads();
 
@@ -444,18 +418,20 @@ __global__ __launch_bounds__(64 * GNL_WAVES, 1) void gn_linear_kernel(
     for (int j = 0; j < NT; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      float rs[GPC], nm[GPC];
-#pragma unroll
-      for (int k = 0; k < GPC; ++k) {
-        rs[k] = sv[s][k].y;
-        nm[k] = -sv[s][k].x * sv[s][k].y;
-      }
+      const int c8 = (4 * s + q) * 8;  // first channel of this lane's chunk
+      const float4 g0 = *reinterpret_cast<const float4*>(&sg[c8]), g1 = *reinterpret_cast<const float4*>(&sg[c8 + 4]);
+      const float4 e0 = *reinterpret_cast<const float4*>(&sbe[c8]), e1 = *reinterpret_cast<const float4*>(&sbe[c8 + 4]);
+      const float ga[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float be[8] = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
       const unsigned xv[4] = {xb[s].x, xb[s].y, xb[s].z, xb[s].w};
       unsigned zv[4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {  // v_fma_mix_f32 on the packed fp16 pairs, one rounding to fp16
-        const float lo = fma_mix_lo(rs[(2 * p) / CG], xv[p], nm[(2 * p) / CG]);
-        const float hi = fma_mix_hi(rs[(2 * p + 1) / CG], xv[p], nm[(2 * p + 1) / CG]);
+      for (int p = 0; p < 4; ++p) {  // gn_apply's z = fp16(fma(x, sc, of)), the fma on the packed fp16 x
+        const float2 m0 = sv[s][(2 * p) / CG], m1 = sv[s][(2 * p + 1) / CG];  // (mean, rstd)
+        const float sc0 = mul_f32(m0.y, ga[2 * p]), sc1 = mul_f32(m1.y, ga[2 * p + 1]);
+        const float of0 = fma_f32(-m0.x, sc0, be[2 * p]), of1 = fma_f32(-m1.x, sc1, be[2 * p + 1]);
+        const float lo = fma_mix_lo(sc0, xv[p], of0);
+        const float hi = fma_mix_hi(sc1, xv[p], of1);
         typedef float f2v __attribute__((ext_vector_type(2)));
         zv[p] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{lo, hi}, h2));
       }
@@ -605,8 +581,7 @@ bool gnl_fused(int32_t C, int32_t groups, int32_t N) {
 int64_t gnl_stats_bytes(int32_t F, int32_t S, int32_t C, int32_t groups) {
   return (vda_groupnorm_workspace(F, S, C, groups) * 4 + 255) / 256 * 256;
 }
-// fused route: [GroupNorm partials + (mean, rstd)] [W' half N x C] [b' float N]
-int64_t gnl_fold_bytes(int32_t C, int32_t N) { return ((int64_t)N * C * 2 + (int64_t)N * 4 + 255) / 256 * 256; }
+
 }  // namespace
 
 extern "C" int vda_groupnorm_linear_fused(int32_t C, int32_t groups, int32_t N) { return gnl_fused(C, groups, N) ? 1 : 0; }
@@ -614,8 +589,7 @@ extern "C" int vda_groupnorm_linear_fused(int32_t C, int32_t groups, int32_t N) 
 extern "C" int64_t vda_groupnorm_linear_workspace(int32_t F, int32_t S, int32_t C, int32_t groups, int32_t N) {
   if (F <= 0 || S <= 0 || C <= 0 || groups <= 0 || N <= 0) return 0;
   const int64_t b = gnl_stats_bytes(F, S, C, groups);
-  return gnl_fused(C, groups, N) ? b + gnl_fold_bytes(C, N)
-                                 : b + (int64_t)F * S * C * 2;  // the normalised copy of x (unfused route)
+  return gnl_fused(C, groups, N) ? b : b + (int64_t)F * S * C * 2;  // + the normalised copy of x (unfused route)
 }
 
 extern "C" int vda_groupnorm_linear(const void* x, const float* gamma, const float* beta, int32_t F, int32_t S,
@@ -643,20 +617,14 @@ extern "C" int vda_groupnorm_linear(const void* x, const float* gamma, const flo
   }
   const int nchunk = (S + gn_rows(C) - 1) / gn_rows(C);
   float* stats = wsf + 2L * F * nchunk * C;
-  h16* wf = (h16*)((char*)ws + gnl_stats_bytes(F, S, C, groups));
-  float* bf = (float*)(wf + (long)N * C);
-  const int npart = F * nchunk;
   const int ntiles = (M + 15) / 16;
   const int nblk = std::min(vda_cu_count(), (ntiles + GNL_WAVES - 1) / GNL_WAVES);
-#define VDA_GNL(KK)                                                                                                  \
-  do {                                                                                                               \
-    hipLaunchKernelGGL(gnl_prep_kernel<KK>, dim3(npart + gnl_fold_blocks<KK>()), dim3(256), 0, st, (const h16*)x, wsf, \
-                       S, C, groups, nchunk, npart, (const h16*)w, gamma, beta, bias, wf, bf);                           \
-    hipLaunchKernelGGL(gn_finalize_kernel, dim3(F * groups), dim3(64), 0, st, (const h16*)x, (const float*)wsf, stats, \
-                       S, C, groups, nchunk, eps);                                                                   \
-    hipLaunchKernelGGL(gn_linear_kernel<KK>, dim3(nblk), dim3(64 * GNL_WAVES), 0, st, (const h16*)x,                  \
-                       (const float*)stats, (const h16*)wf, (const float*)bf, (h16*)y, stats_out, M, S, ntiles);     \
-  } while (0)
+  hipLaunchKernelGGL(gn_partial_kernel, dim3(F * nchunk), dim3(256), 0, st, (const h16*)x, wsf, S, C, groups, nchunk);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(F * groups), dim3(64), 0, st, (const h16*)x, (const float*)wsf, stats, S,
+                     C, groups, nchunk, eps);
+#define VDA_GNL(KK)                                                                                                 \
+  hipLaunchKernelGGL(gn_linear_kernel<KK>, dim3(nblk), dim3(64 * GNL_WAVES), 0, st, (const h16*)x, (const float*)stats, \
+                     (const h16*)w, gamma, beta, bias, (h16*)y, stats_out, M, S, ntiles)
   if (C == 256)
     VDA_GNL(256);
   else if (C == 128)
