@@ -97,6 +97,14 @@ typedef struct vda_epilogue {
    * by two launches that can run at the same time (one per stream).  NULL: static schedule.  Ignored by
    * the other kernel routes. */
   int32_t* sched;
+  /* drop_period > 0 (vda_gemm only): X is a token stream of frames of drop_period rows whose first row is
+   * the cls token (the encoder output, dinov2.py:309-312 get_intermediate_layers drops it); output rows
+   * m with m % drop_period == 0 are not stored and row m goes to Y row m - m / drop_period - 1, so Y
+   * holds the M - ceil(M / drop_period) patch rows.  For the DPT projects 1x1 conv on a tap with the
+   * final LayerNorm folded in (dpt.py:60-68).  Served by the phased route's register epilogue only:
+   * drop_period >= 256, ln_stats + ln_colsum + bias, activation none, row store, no gamma / res / res2 /
+   * rowbias / stats_out, N % 256 == 0, M >= 4096, K % 64 == 0, 16-byte aligned Y rows; -22 otherwise. */
+  int32_t drop_period;
 } vda_epilogue;
 
 /* Version / diagnostics. */

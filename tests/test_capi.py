@@ -174,6 +174,8 @@ def test_torch_ops_registered_meta_shapes_and_no_cpu_kernel():
     assert up.shape == (2, 20, 24, 32)
     o = torch.empty(100, 96, device="meta", dtype=torch.float16)
     assert torch.ops.vda.gemm.out(x, w, act=0, out=o) is not None
+    assert torch.ops.vda.gemm(torch.empty(2740, 64, device="meta", dtype=torch.float16), w,
+                              drop_period=1370).shape == (2738, 96)  # the two cls rows left out
     g = x.new_empty(64, dtype=torch.float32)
     assert torch.ops.vda.groupnorm_linear(x, g, g, 4, 32, 1e-6, w, None).shape == (100, 96)
     with pytest.raises(NotImplementedError):

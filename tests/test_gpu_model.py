@@ -69,6 +69,27 @@ def test_forward_ff_norm_fold_matches_oracle(enc, T, H, W):
     assert rel_l1(d1, d0) < 1e-3
 
 
+def test_forward_tap_norm_fold():
+    """fold_tap_norm (on by default): each encoder tap's final LayerNorm folded into its DPT projects GEMM, the
+    cls rows dropped in that GEMM's store (vda.h drop_period).  ViT-L at 12 x 266^2 (362 tokens per frame,
+    4,344 rows: the phased route serves it); the forward with the fold differs from the LayerNorm + GEMM
+    forward only by fp16 rounding (bar 1e-3 rel-L1; the full-size parity tests cover it against the oracle)."""
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(1, 12, 3, 266, 266, generator=g).cuda()
+    m = model("vitl")
+    P = m._pack(x.device)
+    assert m._tap_fold(P, 12, 362) and not m._tap_fold(P, 4, 362)
+    d1 = m(x).float().cpu()
+    m.fold_tap_norm = False
+    try:
+        d0 = m(x).float().cpu()
+    finally:
+        m.fold_tap_norm = True
+    err = rel_l1(d1, d0)
+    print(f"vitl 1x12x266x266: fold_tap_norm vs LayerNorm + GEMM rel-L1 {err:.3e}")
+    assert err < 1e-3
+
+
 def test_forward_deterministic_and_batch_independent():
     """Clip-parallel sharding relies on per-clip independence: B=2 == two B=1 runs."""
     g = torch.Generator().manual_seed(3)

@@ -276,6 +276,51 @@ def test_groupnorm_linear_large_rows():
     assert torch.equal(y, unf)
 
 
+@pytest.mark.parametrize("BT,ntok,C,N,parts", [(4, 1370, 1024, 256, 0), (4, 1370, 1024, 512, 4), (12, 362, 384, 256, 0),
+                                               (3, 1370, 1024, 1024, 4)])
+def test_gemm_ln_fold_drop_period(BT, ntok, C, N, parts):
+    """The DPT projects GEMM on an encoder tap with the final LayerNorm folded in and the cls rows dropped in the
+    store (vda.h drop_period; dinov2.py:309-312 + dpt.py:60-68) against LayerNorm(skip_period) + GEMM: same
+    rows, rel-L1 < 2e-3 (the fold's fp32 epilogue vs the fp16 normalised copy).  Statistics as row_stats
+    ([M, 2]) or as 256-column partial sums ([M, P, 2], what the fc2 epilogue writes).  Frames of 1,370 and
+    362 rows: tiles that start on a cls row, tiles crossing a frame boundary, a ragged last tile."""
+    M = BT * ntok
+    torch.manual_seed(5)
+    x = (torch.randn(M, C, device=DEV) * 2 + 0.5).half()
+    x[::97, :8] += 30.0  # a few rows with large channels (the residual stream's massive activations)
+    gam = torch.rand(C, device=DEV) + 0.5
+    bet = torch.randn(C, device=DEV) * 0.1
+    w = torch.randn(N, C, device=DEV) * C ** -0.5
+    b = torch.randn(N, device=DEV) * 0.1
+    wg = (w * gam[None, :]).half()
+    c1 = wg.float().sum(1)
+    bb = w @ bet + b
+    if parts:
+        xf = x.float().view(M, parts, C // parts)
+        st = torch.stack([xf.sum(-1), (xf * xf).sum(-1)], -1).contiguous()
+    else:
+        st = ops.row_stats(x, 1e-6)
+    y = ops.gemm(x, wg, bias=bb, ln_stats=st, ln_parts=parts, ln_eps=1e-6, ln_colsum=c1, drop_period=ntok)
+    assert y.shape == (BT * (ntok - 1), N)
+    ref = ops.gemm(ops.layernorm(x, gam, bet, 1e-6, skip_period=ntok - 1), w.half(), bias=b)
+    assert rel(y, ref) < 2e-3
+    t = ops.layernorm(x, gam, bet, 1e-6).float().view(BT, ntok, C)[:, 1:].reshape(-1, C) @ w.half().float().t() + b
+    assert rel(y, t) < 2e-3
+
+
+def test_gemm_drop_period_validation():
+    """drop_period is served by the phased route's LN-fold register epilogue only: other shapes are refused."""
+    x = torch.zeros(4 * 362, 384, device=DEV, dtype=torch.float16)  # M = 1,448 < 4,096
+    w = torch.zeros(256, 384, device=DEV, dtype=torch.float16)
+    st = ops.row_stats(x, 1e-6)
+    c1, bb = torch.zeros(256, device=DEV), torch.zeros(256, device=DEV)
+    with pytest.raises(RuntimeError, match="drop_period"):
+        ops.gemm(x, w, bias=bb, ln_stats=st, ln_colsum=c1, drop_period=362)
+    x = torch.zeros(32 * 141, 384, device=DEV, dtype=torch.float16)  # frames of 141 rows < 256
+    with pytest.raises(RuntimeError, match="drop_period"):
+        ops.gemm(x, w, bias=bb, ln_stats=ops.row_stats(x, 1e-6), ln_colsum=c1, drop_period=141)
+
+
 @pytest.mark.parametrize("B,N,H", [(2, 200, 3), (1, 1370, 16), (3, 82, 6), (1, 64, 1)])
 def test_spatial_attention(B, N, H):
     D = 64

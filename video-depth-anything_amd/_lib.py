@@ -55,6 +55,7 @@ class Epilogue(ctypes.Structure):
         ("ps_cout", c_int32), ("ps_hin", c_int32), ("ps_win", c_int32),
         ("ln_stats", c_void_p), ("ln_colsum", c_void_p), ("ln_parts", c_int32), ("ln_eps", c_float),
         ("stats_out", c_void_p), ("res2_h", c_int32), ("res2_w", c_int32), ("sched", c_void_p),
+        ("drop_period", c_int32),
     ]
 
 

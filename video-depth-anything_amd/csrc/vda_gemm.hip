@@ -1206,10 +1206,25 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
     TS(4);
     static_assert(phased_nit<XR, WR, ACT>() == 16, "the register epilogue issues 16 stores per lane");
     const int g = lane >> 4;
-    const long mrows = p.M - m0;
+    // row drop (vda_epilogue.drop_period, the projects GEMM on a tap with the cls rows left out): source
+    // row m0 + r of frame f goes to Y row m0 + r - f - 1, the frame's first row nowhere.  drop_period >= 256,
+    // so a tile meets at most one frame boundary (tile row rbd).  Y base row ybase = Y row of m0 (or 0).
+    const int dp = e.drop_period;
+    const int f0 = dp > 0 ? m0 / dp : 0;
+    const int rbd = dp > 0 ? (f0 + 1) * dp - m0 : 1 << 30;
+    const bool cls0 = dp > 0 && m0 % dp == 0;
+    const long ybase = dp > 0 ? (m0 - f0 - (cls0 ? 0 : 1)) : m0;
+    const long yrows = dp > 0 ? (long)p.M - (p.M + dp - 1) / dp : p.M;
+    const long mrows = yrows - ybase;
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(p.y + (long)m0 * p.ldy), (short)0,
+        (void*)(p.y + ybase * p.ldy), (short)0,
         (int)(mrows * p.ldy * 2 < 0x7fffffffL ? mrows * p.ldy * 2 : 0x7fffffffL), 0x00020000);
+    // byte offset of tile row r in ry (0x80000000: not stored)
+    auto yrow = [&](int r) -> unsigned {
+      if (dp == 0) return (unsigned)(r * p.ldy * 2);
+      if ((cls0 && r == 0) || r == rbd) return 0x80000000u;
+      return (unsigned)((m0 + r - f0 - (r > rbd ? 2 : 1) - ybase) * p.ldy * 2);
+    };
     unsigned cofs[2];
 #pragma unroll
     for (int pp = 0; pp < 2; ++pp) {
@@ -1275,8 +1290,11 @@ __device__ __forceinline__ int gemm256_tile(const GemmParams& p, int vb, int til
         A[k] = lo8 ? o[0][k] : got;
         B[k] = lo8 ? got : o[1][k];
       }
-      const unsigned rA = (unsigned)((wm * 128 + j * 16 + (mcol & 7)) * p.ldy * 2) + (lo8 ? cofs[0] : cofs[1]);
-      const unsigned rB = rA + (unsigned)(8 * p.ldy * 2);
+      const int ra = wm * 128 + j * 16 + (mcol & 7);
+      const unsigned co = lo8 ? cofs[0] : cofs[1];  // N % 256 == 0 with drop_period: never the sentinel
+      const unsigned ya = yrow(ra), yb = yrow(ra + 8);
+      const unsigned rA = ya == 0x80000000u ? ya : ya + co;
+      const unsigned rB = yb == 0x80000000u ? yb : yb + co;
       __builtin_amdgcn_raw_buffer_store_b128(A, ry, rA, 0, VDA_EPI_STORE_AUX);
       __builtin_amdgcn_raw_buffer_store_b128(B, ry, rB, 0, VDA_EPI_STORE_AUX);
     }
@@ -2072,6 +2090,15 @@ extern "C" int vda_gemm(const void* x, int64_t ldx, const void* w, void* y, int6
   if (p.epi.rdiv <= 0) p.epi.rdiv = 1;
   if (p.epi.rmod <= 0) p.epi.rmod = 1;
   VDA_CHECK_ARG(p.epi.res2_h == 0 && p.epi.res2_w == 0, "upsampled res2: vda_conv2d only");
+  if (p.epi.drop_period != 0) {  // only the phased route's register LN-fold epilogue (EK 1) drops rows
+    const vda_epilogue& e = p.epi;
+    VDA_CHECK_ARG(e.drop_period >= 256 && e.ln_stats && e.ln_colsum && e.bias && e.act == VDA_ACT_NONE &&
+                      e.store == VDA_STORE_ROWS && !e.gamma && !e.res && !e.res2 && !e.rowbias && !e.stats_out &&
+                      N % 256 == 0 && M >= 4096 && K % 64 == 0 && (long)M * ldx * 2 < (1L << 31) &&
+                      (long)N * K * 2 < (1L << 31) && (uintptr_t)y % 16 == 0 && ldy % 8 == 0 && g_force_tile < 0,
+                  "drop_period: >= 256, with ln_stats + bias, no activation / gamma / res / rowbias / stats_out, "
+                  "N % 256 == 0, M >= 4096, K % 64 == 0, 16-byte aligned rows");
+  }
   int rc = check_epi(p.epi, M, N);
   if (rc) return rc;
   if (p.epi.ln_stats && p.epi.rowbias) {  // only the phased 256x256 route (EK 3) implements the pair

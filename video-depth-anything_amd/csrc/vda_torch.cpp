@@ -111,18 +111,23 @@ vda_epilogue make_epi(const Tensor& x, OptT bias, OptT rowbias, int64_t rdiv, in
 }
 
 // ---- linear / 1x1 conv / ConvTranspose(k=s) ------------------------------------------------------
+// rows of the GEMM output: M, or M - ceil(M / drop_period) with the cls rows dropped (vda.h drop_period)
+int64_t gemm_out_rows(int64_t M, int64_t drop_period) { return drop_period > 0 ? M - (M + drop_period - 1) / drop_period : M; }
+
 Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
                  OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-                 OptT stats_out, OptT sched, Tensor out) {
+                 OptT stats_out, OptT sched, int64_t drop_period, Tensor out) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "vda gemm: x must be a 2-D row-major (possibly row-strided) matrix");
   need_contig(w, dt, "w", x);
   TORCH_CHECK(w.dim() == 2 && w.size(1) == x.size(1), "vda gemm: K mismatch ", w.sizes(), " vs ", x.sizes());
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   const int64_t nout = act == VDA_ACT_GEGLU ? N / 2 : N;
-  TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == nout && out.stride(1) == 1 &&
+  TORCH_CHECK(drop_period >= 0, "vda gemm: drop_period >= 0");
+  const int64_t Mo = gemm_out_rows(M, drop_period);
+  TORCH_CHECK(out.dim() == 2 && out.size(0) == Mo && out.size(1) == nout && out.stride(1) == 1 &&
                   out.scalar_type() == dt && out.device() == x.device(),
-              "vda gemm: out must be [", M, ", ", nout, "] ", dt, " with unit column stride");
+              "vda gemm: out must be [", Mo, ", ", nout, "] ", dt, " with unit column stride");
   if (stats_out)
     TORCH_CHECK(stats_out->dim() == 3 && stats_out->size(0) >= M && stats_out->size(1) == (nout + 255) / 256 &&
                     stats_out->size(2) == 2 && stats_out->scalar_type() == at::kFloat && stats_out->is_contiguous(),
@@ -136,6 +141,7 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
     TORCH_CHECK(sched->numel() >= 9, "vda gemm: sched must hold >= 9 int32 counters");
     e.sched = (int32_t*)sched->data_ptr();
   }
+  e.drop_period = (int32_t)drop_period;
   const int rc = dt == at::kHalf
                      ? vda_gemm(x.data_ptr(), x.stride(0), w.data_ptr(), out.data_ptr(), out.stride(0), (int32_t)M,
                                 (int32_t)N, (int32_t)K, &e, stream_of(x))
@@ -148,20 +154,20 @@ Tensor gemm_into(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int6
 
 Tensor gemm(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
             OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-            OptT stats_out, OptT sched) {
+            OptT stats_out, OptT sched, int64_t drop_period) {
   const auto dt = act_dtype(x);
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2, "vda gemm: x and w must be 2-D");
   const int64_t nout = act == VDA_ACT_GEGLU ? w.size(0) / 2 : w.size(0);
-  Tensor out = at::empty({x.size(0), nout}, x.options().dtype(dt));
+  Tensor out = at::empty({gemm_out_rows(x.size(0), drop_period), nout}, x.options().dtype(dt));
   return gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps,
-                   stats_out, sched, out);
+                   stats_out, sched, drop_period, out);
 }
 
 Tensor& gemm_out(const Tensor& x, const Tensor& w, OptT bias, OptT rowbias, int64_t rdiv, int64_t rmod, OptT gamma,
                  OptT res, OptT res2, int64_t act, OptT ln_stats, OptT ln_colsum, int64_t ln_parts, double ln_eps,
-                 OptT stats_out, OptT sched, Tensor& out) {
+                 OptT stats_out, OptT sched, int64_t drop_period, Tensor& out) {
   gemm_into(x, w, bias, rowbias, rdiv, rmod, gamma, res, res2, act, ln_stats, ln_colsum, ln_parts, ln_eps, stats_out,
-            sched, out);
+            sched, drop_period, out);
   return out;
 }
 
@@ -500,11 +506,11 @@ TORCH_LIBRARY(vda, m) {
   m.def("gemm(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
         "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, "
-        "Tensor(c!)? sched=None) -> Tensor");
+        "Tensor(c!)? sched=None, int drop_period=0) -> Tensor");
   m.def("gemm.out(Tensor x, Tensor w, Tensor? bias=None, Tensor? rowbias=None, int rdiv=1, int rmod=1, "
         "Tensor? gamma=None, Tensor? res=None, Tensor? res2=None, int act=0, Tensor? ln_stats=None, "
         "Tensor? ln_colsum=None, int ln_parts=0, float ln_eps=1e-6, Tensor(b!)? stats_out=None, "
-        "Tensor(c!)? sched=None, *, Tensor(a!) out) -> Tensor(a!)");
+        "Tensor(c!)? sched=None, int drop_period=0, *, Tensor(a!) out) -> Tensor(a!)");
   m.def("row_stats(Tensor x, float eps) -> Tensor");
   m.def("conv_transpose_ks(Tensor x, Tensor w, Tensor bias, int BT, int h, int w_, int k) -> Tensor");
   m.def("conv2d(Tensor x, Tensor w, int ks=3, int stride=1, int pad=1, Tensor? bias=None, bool pre_relu=False, "

@@ -240,7 +240,8 @@ class VideoDepthAnything(nn.Module):
     proj / fc2 epilogues instead of a separate pass, ``fold_ff_norm`` folds the motion modules' ff_norm into
     their GEGLU GEMM (fp16 mode, with ``fold_layernorms``), ``fuse_groupnorm_linear`` runs each motion
     module's GroupNorm + proj_in as the one ``groupnorm_linear`` op (the normalised input never written),
-    ``dynamic_tiles`` lets the encoder's persistent GEMMs
+    ``fold_tap_norm`` folds the final LayerNorm of each encoder tap into its DPT projects GEMM (the cls rows
+    dropped in that GEMM's store), ``dynamic_tiles`` lets the encoder's persistent GEMMs
     take their tiles by atomic ticket (per-stream counters, ``ops.sched_counters``) instead of a fixed
     stride.  No environment variable changes the schedule."""
 
@@ -249,6 +250,7 @@ class VideoDepthAnything(nn.Module):
     dynamic_tiles: bool = False
     fold_ff_norm: bool = False  # built and tested; same-box forward A/B 693.7 -> 690.0 frames/s (r06_ab_ffold.log)
     fuse_groupnorm_linear: bool = True
+    fold_tap_norm: bool = True
 
     def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
                  use_clstoken=False, num_frames=32, pe="ape"):
@@ -312,18 +314,18 @@ class VideoDepthAnything(nn.Module):
         # normalised copy of the token tensor is never written or re-read.
         P.lnfold = not fp32 and bool(self.fold_layernorms)
 
-        def _ln_fold(lin, ln):
-            w = lin.weight.detach().float()
+        def _ln_fold(weight, bias, ln):
+            w = weight.detach().float()
             wg = (w * ln.weight.detach().float()[None, :]).to(wd).contiguous()
             c1 = wg.float().sum(1).contiguous()
-            bb = (w @ ln.bias.detach().float() + lin.bias.detach().float()).contiguous()
+            bb = (w @ ln.bias.detach().float() + bias.detach().float()).contiguous()
             return wg.to(dev), c1.to(dev), bb.to(dev)
 
         for b in enc.blocks:
             q = _Packed()
             q.n1w, q.n1b = _f(b.norm1.weight).to(dev), _f(b.norm1.bias).to(dev)
             if P.lnfold:
-                q.qkv_w, q.qkv_c1, q.qkv_b = _ln_fold(b.attn.qkv, b.norm1)
+                q.qkv_w, q.qkv_c1, q.qkv_b = _ln_fold(b.attn.qkv.weight, b.attn.qkv.bias, b.norm1)
             else:
                 q.qkv_w, q.qkv_b = _h(b.attn.qkv.weight).to(dev), _f(b.attn.qkv.bias).to(dev)
             # LayerScale folded into the projections (gamma * (W h + b) = (gamma W) h + gamma b): the
@@ -333,7 +335,7 @@ class VideoDepthAnything(nn.Module):
             q.proj_b = _f(b.attn.proj.bias.detach().float() * g1).to(dev)
             q.n2w, q.n2b = _f(b.norm2.weight).to(dev), _f(b.norm2.bias).to(dev)
             if P.lnfold:
-                q.fc1_w, q.fc1_c1, q.fc1_b = _ln_fold(b.mlp.fc1, b.norm2)
+                q.fc1_w, q.fc1_c1, q.fc1_b = _ln_fold(b.mlp.fc1.weight, b.mlp.fc1.bias, b.norm2)
             else:
                 q.fc1_w, q.fc1_b = _h(b.mlp.fc1.weight).to(dev), _f(b.mlp.fc1.bias).to(dev)
             g2 = b.ls2.gamma.detach().float()
@@ -352,6 +354,10 @@ class VideoDepthAnything(nn.Module):
                 P.ro_b.append(_f(rp[0].bias).to(dev))
         P.proj_w = [_h(c.weight.reshape(c.weight.shape[0], -1)).to(dev) for c in hd.projects]
         P.proj_b = [_f(c.bias).to(dev) for c in hd.projects]
+        # the final LayerNorm of each tap (dinov2.py:310) folded into its projects 1x1 conv (dpt.py:60-68)
+        # the same way: the tap's normalised copy is never written (used when _tap_fold says so)
+        if P.lnfold and not self.use_clstoken:
+            P.projf = [_ln_fold(c.weight.reshape(c.weight.shape[0], -1), c.bias, enc.norm) for c in hd.projects]
         P.rs_w, P.rs_b = {}, {}
         for i, k in ((0, 4), (1, 2)):
             ct = hd.resize_layers[i]
@@ -569,6 +575,8 @@ class VideoDepthAnything(nn.Module):
             st_b = torch.empty_like(st_a)
         stats, parts = None, 0
         sch = ops.sched_counters(tok.device) if self.dynamic_tiles and P.dt == torch.float16 else None
+        # taps straight into their LN-folded projects GEMM, cls rows dropped in its store (vda.h drop_period)
+        tapfold = epistats and self._tap_fold(P, BT, ntok)
         for i, q in enumerate(P.blocks):
             if P.lnfold:  # norm1 folded into the qkv GEMM (statistics only)
                 if stats is None:
@@ -591,20 +599,31 @@ class VideoDepthAnything(nn.Module):
                 f = ops.gemm(ops.layernorm(tok, q.n2w, q.n2b, 1e-6), q.fc1_w, bias=q.fc1_b, act=ACT_GELU,
                              tag="enc_fc1")
             last = i + 1 == len(P.blocks)
-            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok, stats_out=st_b if epistats and not last else None,
-                     sched=sch)
+            ops.gemm(f, q.fc2_w, bias=q.fc2_b, res=tok, out=tok,
+                     stats_out=st_b if epistats and (not last or (tapfold and i in taps)) else None, sched=sch)
             stats, parts = (st_b, nparts) if epistats else (None, 0)
             del f
-            if i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
+            if i in taps and tapfold:  # projects(norm(tap)) with the cls rows left out (dinov2.py:309-312)
+                w_, c1_, b_ = P.projf[len(feats)]
+                feats.append(ops.gemm(tok, w_, bias=b_, ln_stats=st_b, ln_parts=nparts, ln_eps=1e-6, ln_colsum=c1_,
+                                      drop_period=ntok))
+            elif i in taps:  # final norm on the tap, cls row dropped (dinov2.py:309-312)
                 feats.append(ops.layernorm(tok, P.nw, P.nb, 1e-6, skip_period=npt))
                 if cls is not None:  # the same norm on each frame's cls row (row stride ntok*C)
                     cls.append(ops.layernorm(tok.view(BT, ntok, -1)[:, 0], P.nw, P.nb, 1e-6))
-        return feats, cls
+        return feats, cls, tapfold
+
+    def _tap_fold(self, P: _Packed, BT: int, ntok: int) -> bool:
+        """Whether the taps go straight into their LN-folded projects GEMMs: the shapes the phased GEMM's
+        row-drop epilogue serves (vda.h drop_period), fp16, no readout."""
+        if not (P.lnfold and bool(self.fold_tap_norm) and getattr(P, "projf", None) is not None):
+            return False
+        return ntok >= 256 and BT * ntok >= 4096 and P.C % 64 == 0 and all(w.shape[0] % 256 == 0 for w, _, _ in P.projf)
 
     def _reassemble(self, P: _Packed, enc, BT: int, ph: int, pw: int) -> List[torch.Tensor]:
         """DPT reassemble (dpt_temporal.py:55-69 == get_motion_features :101-131, dpt.py:60-90):
         enc = _encode's (taps, cls) -> layer_1..4 NHWC [BT, h, w, C]."""
-        feats, cls = enc
+        feats, cls, projected = enc
         oc = self.out_channels
         lay = []
         for i, ft in enumerate(feats):
@@ -613,7 +632,7 @@ class VideoDepthAnything(nn.Module):
                 # term is one fp32 row per frame, a row bias of the patch GEMM
                 rb = ops.gemm(cls[i].float(), P.ro_wb[i], bias=P.ro_b[i])
                 ft = ops.gemm(ft, P.ro_wa[i], rowbias=rb, rdiv=ph * pw, rmod=BT, act=ACT_GELU)
-            p = ops.gemm(ft, P.proj_w[i], bias=P.proj_b[i])
+            p = ft if projected else ops.gemm(ft, P.proj_w[i], bias=P.proj_b[i])
             if i == 0:
                 l = ops.conv_transpose_ks(p, P.rs_w[0], P.rs_b[0], BT, ph, pw, 4)
             elif i == 1:

@@ -56,7 +56,7 @@ def _need(t: Tensor, dtype, name: str):
 
 def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma=None, res=None,
          res2=None, act=ACT_NONE, ln_stats=None, ln_colsum=None, ln_parts=0, ln_eps=1e-6, stats_out=None,
-         sched=None, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
+         sched=None, drop_period=0, out: Optional[Tensor] = None, tag: Optional[str] = None) -> Tensor:
     """out[M, N'] = epi(x[M, K] @ w[N, K]^T); N' = N (N/2 for GEGLU). x may be a row-strided view.
     fp16 x/w -> vda_gemm; fp32 x/w -> vda_gemm_f32 (fp32 mode).  torch.ops.vda.gemm[.out].
     ``ln_stats`` + ``ln_colsum`` fold a LayerNorm of x into the GEMM (vda.h): ln_stats is either
@@ -64,7 +64,9 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
     through ``stats_out`` while producing x (ln_parts=P, ln_eps the LayerNorm eps).  ``stats_out``
     ([M, ceil(N/256), 2] fp32) receives this GEMM's per-row partial (sum, sumsq) of its output.
     ``sched`` (int32 [>= 9], zeroed once; see ``sched_counters``) lets the persistent 256x256 GEMM take its
-    tiles by atomic ticket; one counter set per stream (vda.h vda_epilogue.sched)."""
+    tiles by atomic ticket; one counter set per stream (vda.h vda_epilogue.sched).  ``drop_period`` = P > 0:
+    x is frames of P token rows, the first the cls token; the output leaves those rows out
+    ([M - ceil(M / P), N'], the LN-folded projects GEMM on an encoder tap, vda.h drop_period)."""
     _need(x, x.dtype, "x")
     probe = _PROBE is not None and tag in _PROBE
     if probe:
@@ -73,10 +75,10 @@ def gemm(x: Tensor, w: Tensor, *, bias=None, rowbias=None, rdiv=1, rmod=1, gamma
     v = _vda()
     if out is None:
         out = v.gemm(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum,
-                     int(ln_parts), float(ln_eps), stats_out, sched)
+                     int(ln_parts), float(ln_eps), stats_out, sched, int(drop_period))
     else:
         v.gemm.out(x, w, bias, rowbias, int(rdiv), int(rmod), gamma, res, res2, int(act), ln_stats, ln_colsum,
-                   int(ln_parts), float(ln_eps), stats_out, sched, out=out)
+                   int(ln_parts), float(ln_eps), stats_out, sched, int(drop_period), out=out)
     if probe:
         ev1.record()
         _PROBE[tag].append((ev0, ev1, 2.0 * x.shape[0] * w.shape[0] * x.shape[1]))
