@@ -35,6 +35,8 @@ int vda_debug_hconv(int32_t mode);
 /* Depth tail: -1 = automatic (the 2-blocks-per-CU depth conv with the resize fused), 2 = the same conv on
  * a materialised resize (bit-identical; needs the workspace), 0 = the older 8-wave halo kernels. */
 int vda_debug_dconv(int32_t mode);
+/* fused depth conv: the second half of its grid starts units1024 x 1024 shader cycles late (0 = off) */
+int vda_debug_dconv_stagger(int32_t units1024);
 /* Attention kernels: spatial 1 = the round-1 16x16x32 kernel; temporal 1 = the direct-load kernel. */
 int vda_debug_attn(int32_t spatial_old, int32_t temporal_old);
 

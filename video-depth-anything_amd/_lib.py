@@ -31,7 +31,8 @@ EXPORTED = (
 )
 # The tuning build (make tune -> build/tune/libvda.so, include/vda_tune.h) adds these.
 TUNE_EXPORTED = ("vda_debug_force_tile", "vda_debug_gemm_sched", "vda_debug_gemm_desync", "vda_debug_gemm_epi",
-                 "vda_debug_strip_split", "vda_debug_hconv", "vda_debug_dconv", "vda_debug_attn")
+                 "vda_debug_strip_split", "vda_debug_hconv", "vda_debug_dconv", "vda_debug_attn",
+                 "vda_debug_dconv_stagger")
 TUNE_LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "tune", "libvda.so")
 
 ACT_NONE, ACT_GELU, ACT_GEGLU, ACT_RELU = 0, 1, 2, 3
@@ -104,6 +105,7 @@ def _declare(lib):
         "vda_debug_strip_split": ([I], I),
         "vda_debug_hconv": ([I], I),
         "vda_debug_dconv": ([I], I),
+        "vda_debug_dconv_stagger": ([I], I),
         "vda_debug_gemm_epi": ([I], I),
         "vda_debug_attn": ([I, I], I),
     }

@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
                                                            const float* __restrict__ b1, const float* __restrict__ w2,
                                                            const float* __restrict__ b2, float* __restrict__ depth,
                                                            int H, int W, int C, int tiles_x, int tiles_y, int ntiles,
-                                                           int Hs, int Ws) {
+                                                           int Hs, int Ws, int stagger) {
   constexpr int DC_WRING = UPS ? 2 : 3;
   __shared__ __attribute__((aligned(1024))) h16 sm[2 * DC_PSLOT + DC_WRING * DC_WROW + (UPS ? DC_SSLOT : 0)];
   h16* const psm = sm;
@@ -256,6 +256,10 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
 #pragma unroll
     for (int m = 0; m < 4; ++m) acc[n][m] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // start stagger (tuning build, vda_debug_dconv_stagger): the second half of the grid - the second block
+  // on each CU - starts `stagger` x 1024 cycles late, so the two blocks' interpolation rows fall out of phase
+  if (stagger > 0 && (int)blockIdx.x >= (int)gridDim.x / 2)
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
   if constexpr (UPS) {
     // prologue: unit 0's source region -> its patch (interpolated), W(0); unit 1's source in flight
     src_dma(0);
@@ -444,6 +448,7 @@ extern "C" int vda_debug_dconv_timestamps(void* host) {
 
 // vda_debug_dconv (tuning build): -1 automatic (fused), 0 never, 2 resize + unfused depth conv
 VDA_KNOB(int, g_dconv_mode, -1);
+VDA_KNOB(int, g_dconv_stagger, 0);  // vda_debug_dconv_stagger
 
 bool vda_depth_conv_serves(int H, int W, int C) { return C % 32 == 0 && C > 0 && H > 0 && W > 0 && g_dconv_mode != 0; }
 
@@ -458,7 +463,7 @@ int vda_depth_conv(const void* U, const void* w1, const float* b1, const float* 
   const int ntiles = (int)nt;
   const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
   hipLaunchKernelGGL(depth_conv_kernel<false>, dim3(grid), dim3(256), 0, st, (const h16*)U, (const h16*)w1, b1, w2, b2,
-                     depth, H, W, C, tiles_x, tiles_y, ntiles, H, W);
+                     depth, H, W, C, tiles_x, tiles_y, ntiles, H, W, 0);
   VDA_LAUNCH_CHECK();
   return 0;
 }
@@ -482,7 +487,7 @@ int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const f
   const int ntiles = (int)nt;
   const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
   hipLaunchKernelGGL(depth_conv_kernel<true>, dim3(grid), dim3(256), 0, st, (const h16*)x, (const h16*)w1, b1, w2, b2,
-                     depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws);
+                     depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws, (int)g_dconv_stagger);
   VDA_LAUNCH_CHECK();
   return 0;
 }
@@ -490,6 +495,10 @@ int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const f
 #ifdef VDA_TUNING
 extern "C" int vda_debug_dconv(int32_t mode) {
   g_dconv_mode = mode;
+  return 0;
+}
+extern "C" int vda_debug_dconv_stagger(int32_t units1024) {
+  g_dconv_stagger = units1024;
   return 0;
 }
 #endif
