@@ -427,6 +427,32 @@ def test_ops_reject_cpu_tensors():
         ops.gemm(torch.zeros(4, 8, dtype=torch.float16), torch.zeros(4, 8, dtype=torch.float16))
 
 
+def test_c_abi_groupnorm_linear_direct():
+    """vda_groupnorm_linear through ctypes with the caller's workspace (as a non-torch host would bind it,
+    INTEGRATION.md) == torch.ops.vda.groupnorm_linear, bitwise, on both routes (fused C = 256; composed
+    C = 256 -> N = 512), with stats_out."""
+    from vda_amd import _lib
+    import vda_amd.torch_ops  # noqa: F401
+    lib = _lib.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    Fr, S, C = 3, 77, 256
+    xh = h(rnd(Fr * S, C, seed=150) + 0.2)
+    g, b = f32(rnd(C, seed=151) * 0.2 + 1), f32(rnd(C, seed=152) * 0.1)
+    for N in (256, 512):
+        wh, bias = h(rnd(N, C, scale=C ** -0.5, seed=153)), f32(rnd(N, scale=0.1, seed=154))
+        nws = lib.vda_groupnorm_linear_workspace(Fr, S, C, 32, N)
+        ws = torch.empty(nws, dtype=torch.uint8, device=DEV)
+        y = torch.empty(Fr * S, N, dtype=torch.float16, device=DEV)
+        so = torch.empty(Fr * S, (N + 255) // 256, 2, device=DEV)
+        rc = lib.vda_groupnorm_linear(xh.data_ptr(), g.data_ptr(), b.data_ptr(), Fr, S, C, 32, 1e-6, wh.data_ptr(),
+                                      bias.data_ptr(), y.data_ptr(), N, so.data_ptr(), ws.data_ptr(), nws, st)
+        assert rc == 0, lib.vda_last_error()
+        so1 = torch.empty_like(so)
+        y1 = torch.ops.vda.groupnorm_linear(xh, g, b, Fr, 32, 1e-6, wh, bias, so1)
+        assert torch.equal(y, y1) and torch.equal(so, so1)
+        assert lib.vda_groupnorm_linear_fused(C, 32, N) == (1 if N == C else 0)
+
+
 def test_c_abi_direct_matches_torch_ops():
     """The C ABI called straight through ctypes (as a non-torch host would) == torch.ops.vda.* (the native
     TORCH_LIBRARY registration over the same entry points), bitwise."""
