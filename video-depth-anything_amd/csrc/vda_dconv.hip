@@ -438,272 +438,6 @@ __global__ __launch_bounds__(256, 2) void depth_conv_kernel(const h16* __restric
 #endif
 }
 
-// Interpolation-wave variant of depth_conv_kernel<true> (verdict r5 item 2; tuning build: vda_debug_dconv(3)).
-// Blocks of 6 waves, two per CU (three waves per SIMD, so <= 168 VGPRs): waves 0-3 are the MFMA waves of
-// the kernel above without any interpolation work - the W fragments single-buffered (a tap's next W
-// fragment is read into a register once its 4 MFMAs are issued), the patch read offsets formed per read
-// instead of an 18-register table, the epilogue constants loaded at the epilogue; waves 4-5 own the
-// source staging and the interpolation: right after unit u's first barrier they build unit u+1's patch
-// from the staged source region (the same separable blend, item for item: bit-identical), and after the
-// second they issue unit u+2's source region, which has two rows to land.
-constexpr int DCI_WAVES = 6;
-__global__ __launch_bounds__(64 * DCI_WAVES, 3) void depth_conv_iw_kernel(
-    const h16* __restrict__ U, const h16* __restrict__ w1, const float* __restrict__ b1, const float* __restrict__ w2,
-    const float* __restrict__ b2, float* __restrict__ depth, int H, int W, int C, int tiles_x, int tiles_y, int ntiles,
-    int Hs, int Ws) {
-  __shared__ __attribute__((aligned(1024))) h16 sm[2 * DC_PSLOT + 2 * DC_WROW + DC_SSLOT];
-  h16* const psm = sm;
-  h16* const wsm = sm + 2 * DC_PSLOT;
-  h16* const ssm = sm + 2 * DC_PSLOT + 2 * DC_WROW;  // source region [px][4 chunks]
-  int tid;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(tid) : "v"((int)threadIdx.x));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nslab = C / 32;
-  const int my_tiles = (int)blockIdx.x < ntiles ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int my_units = my_tiles * nslab;
-  if (my_units == 0) return;
-  const int G = my_units * 3;
-  const long K = 9L * C;
-  auto tile_of = [&](int i, int& bt, int& y0, int& x0) __attribute__((always_inline)) {
-    const int t = blockIdx.x + i * gridDim.x;
-    const int tx = t % tiles_x, r = t / tiles_x;
-    y0 = (r % tiles_y) * DC_T;
-    x0 = tx * DC_T;
-    bt = r / tiles_y;
-  };
-
-  if (wave >= 4) {  // ---- interpolation waves ----
-    const int iw = wave - 4;
-    const long fr_halfs = (long)Hs * Ws * C;
-    const float usy = H > 1 ? (float)(Hs - 1) / (float)(H - 1) : 0.f;
-    const float usx = W > 1 ? (float)(Ws - 1) / (float)(W - 1) : 0.f;
-    auto src_region = [&](int y0, int x0, int& sy_lo, int& sx_lo, int& SR, int& SC) __attribute__((always_inline)) {
-      sy_lo = (int)(usy * (float)max(y0 - 1, 0));
-      sx_lo = (int)(usx * (float)max(x0 - 1, 0));
-      SR = min((int)(usy * (float)min(y0 + DC_T, H - 1)) + 1, Hs - 1) - sy_lo + 1;
-      SC = min((int)(usx * (float)min(x0 + DC_T, W - 1)) + 1, Ws - 1) - sx_lo + 1;
-    };
-    auto src_dma = [&](int u) __attribute__((always_inline)) {  // the 12 one-KiB pieces of unit u's source region, 6 per wave
-      int bt, y0, x0, sy_lo, sx_lo, SR, SC;
-      tile_of(u / nslab, bt, y0, x0);
-      src_region(y0, x0, sy_lo, sx_lo, SR, SC);
-      const int slab = u - (u / nslab) * nslab;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(U + bt * fr_halfs), (short)0, (int)(fr_halfs * 2), 0x00020000);
-#pragma unroll
-      for (int j = 0; j < DC_SRCP / 2; ++j) {
-        const int q = iw * (DC_SRCP / 2) + j;
-        const int sl = q * 64 + lane;
-        const int px = sl >> 2;
-        const int r = px / SC, c = px - r * SC;
-        const unsigned vo = r < SR ? (unsigned)((((sy_lo + r) * Ws + sx_lo + c) * C + (sl & 3) * 8) * 2) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (VDA_LDS void*)(ssm + q * 512), 16, (int)vo, slab * 64, 0, 0);
-      }
-    };
-    // one (6-row segment, patch column, channel chunk) item of interp_sep above: items 0..215 =
-    // 3 segments x 18 columns x 4 chunks, the same per-item blend
-    auto interp_item = [&](int u, int it) __attribute__((always_inline)) {
-      int bt, y0, x0, sy_lo, sx_lo, SR, SC;
-      tile_of(u / nslab, bt, y0, x0);
-      src_region(y0, x0, sy_lo, sx_lo, SR, SC);
-      (void)bt; (void)SR;
-      const int seg = it / 72, rem = it - seg * 72;
-      const int px_l = rem >> 2, c = rem & 3;
-      const int pxg = x0 - 1 + px_l;
-      const bool okx = (unsigned)pxg < (unsigned)W;
-      const float ox = (float)min(max(pxg, 0), W - 1);
-      const int sx0 = (int)(usx * ox), sx1 = min(sx0 + 1, Ws - 1);
-      const float wx = ac_weight(usx, ox, sx0), ux = 1.f - wx;
-      const int c0 = sx0 - sx_lo, c1 = sx1 - sx_lo;
-      auto hrow = [&](int sy, float (&t)[8]) {
-        const int r = (sy - sy_lo) * SC;
-        const uint4 a = *reinterpret_cast<const uint4*>(ssm + ((r + c0) * 4 + c) * 8);
-        const uint4 b = *reinterpret_cast<const uint4*>(ssm + ((r + c1) * 4 + c) * 8);
-        const unsigned A[4] = {a.x, a.y, a.z, a.w}, B[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          t[2 * j] = fma_mix_lo(wx, B[j], fma_mix_lo(ux, A[j], -0.f));
-          t[2 * j + 1] = fma_mix_hi(wx, B[j], fma_mix_hi(ux, A[j], -0.f));
-        }
-      };
-      float top[8], bot[8];
-      int s0 = -1, s1 = -1;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        const int pr = seg * 6 + k;
-        const int pyg = y0 - 1 + pr;
-        const float oy = (float)min(max(pyg, 0), H - 1);
-        const int sy0 = (int)(usy * oy), sy1 = min(sy0 + 1, Hs - 1);
-        const float wy = ac_weight(usy, oy, sy0), uy = 1.f - wy;
-        if (sy0 != s0) {
-          if (sy0 == s1) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) top[e] = bot[e];
-          } else {
-            hrow(sy0, top);
-          }
-          hrow(sy1, bot);
-          s0 = sy0;
-          s1 = sy1;
-        }
-        unsigned o[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float ol = fma_f32(wy, bot[2 * j], mul_f32(uy, top[2 * j]));
-          const float oh = fma_f32(wy, bot[2 * j + 1], mul_f32(uy, top[2 * j + 1]));
-          typedef float f2v __attribute__((ext_vector_type(2)));
-          o[j] = __builtin_bit_cast(unsigned, __builtin_convertvector(f2v{ol, oh}, h2));
-        }
-        const bool ok = okx && (unsigned)pyg < (unsigned)H;
-        const uint4 v = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0u, 0u, 0u, 0u);
-        const int p = pr * DC_P + px_l;
-        *reinterpret_cast<uint4*>(psm + (u & 1) * DC_PSLOT + (p * 4 + (c ^ ((p >> 1) & 3))) * 8) = v;
-      }
-    };
-    auto interp = [&](int u) __attribute__((always_inline)) {
-#pragma unroll 1
-      for (int k = 0; k < 2; ++k) {  // one item at a time (registers)
-        const int it = k * 128 + iw * 64 + lane;
-        if (it < 216) interp_item(u, it);
-      }
-    };
-    // The source slot is refilled only after a block barrier that both interpolation waves reach after
-    // their last read of it (each wave's items read pixels of the whole region).
-    src_dma(0);
-    dc_wait<0>();
-    __builtin_amdgcn_s_barrier();  // P1: unit 0's source region landed
-    interp(0);
-    dc_lgkm0();
-    __builtin_amdgcn_s_barrier();  // P2: patch 0 built, the source slot free
-    if (my_units > 1) src_dma(1);
-    dc_wait<0>();  // unit 1's source lands before interp(1), right after barrier 0
-    for (int u = 0; u < my_units; ++u) {
-      for (int dy = 0; dy < 3; ++dy) {
-        __builtin_amdgcn_s_barrier();  // phase 3u + dy
-        if (dy == 0 && u + 1 < my_units) {
-          interp(u + 1);  // patch slot (u + 1) & 1: the MFMA waves finished reading it in unit u - 1
-          dc_lgkm0();     // written (LDS) before barrier 3u + 1
-        }
-        if (dy == 1 && u + 2 < my_units) src_dma(u + 2);  // both waves are past their interp(u + 1) reads
-        if (dy == 2) dc_wait<0>();  // unit u + 2's source lands before interp(u + 2) at the next unit
-      }
-    }
-    return;
-  }
-
-  // ---- MFMA waves ----
-  unsigned wvo[3];
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int k = wave * 3 + j;
-    const int n = (k & 3) * 16 + (lane >> 2);
-    const int cd = (lane & 3) ^ ((n >> 1) & 3);
-    wvo[j] = (unsigned)((n * (int)K + (k >> 2) * C + cd * 8) * 2);
-  }
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)w1, (short)0, (int)(64 * K * 2), 0x00020000);
-  auto w_dma = [&](int g) __attribute__((always_inline)) {  // this wave's 3 pieces of phase g's W slice -> slot g & 1
-    const int u = g / 3, dy = g - u * 3;
-    const int slab = u % nslab;
-    const int so = (dy * 3 * C + slab * 32) * 2;
-#pragma unroll
-    for (int j = 0; j < 3; ++j)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (VDA_LDS void*)(wsm + (g & 1) * DC_WROW + (wave * 3 + j) * 512), 16,
-                                               (int)wvo[j], so, 0, 0);
-  };
-  f4 acc[4][4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n)
-#pragma unroll
-    for (int m = 0; m < 4; ++m) acc[n][m] = f4{0.f, 0.f, 0.f, 0.f};
-  w_dma(0);
-  __builtin_amdgcn_s_barrier();  // P1
-  dc_wait<0>();
-  __builtin_amdgcn_s_barrier();  // P2: W(0) landed, patch 0 built
-  const int frow = lane & 15, g4 = lane >> 4;
-  const int pbase = wave * 4 * DC_P + frow;
-  int wo[4];
-#pragma unroll
-  for (int n = 0; n < 4; ++n) {
-    const int row = n * 16 + frow;
-    wo[n] = (row * 4 + (g4 ^ ((row >> 1) & 3))) * 8;
-  }
-  // X fragment m of tap t at kernel row dy: patch pixel (wave * 4 + m + dy, frow + t)
-  auto xread = [&](const h16* ps, int dy, int t, h8 (&xf)[4]) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int p = pbase + (m + dy) * DC_P + t;
-      xf[m] = *reinterpret_cast<const h8*>(&ps[(p * 4 + (g4 ^ ((p >> 1) & 3))) * 8]);
-    }
-  };
-  for (int u = 0; u < my_units; ++u) {
-    for (int dy = 0; dy < 3; ++dy) {
-      const int g = u * 3 + dy;
-      __builtin_amdgcn_s_barrier();  // phase g: W(g) landed (waited before this barrier), patch u built
-      const bool wnext = g + 1 < G;
-      if (wnext) w_dma(g + 1);  // into the slot phase g - 1 read
-      const h16* ps = psm + (u & 1) * DC_PSLOT;
-      const h16* wb = wsm + (g & 1) * DC_WROW;
-      h8 xa[4], xb[4], wf[4];
-      xread(ps, dy, 0, xa);
-#pragma unroll
-      for (int n = 0; n < 4; ++n) wf[n] = *reinterpret_cast<const h8*>(&wb[wo[n]]);
-      dc_lgkm0();
-      __builtin_amdgcn_sched_barrier(0);
-      xread(ps, dy, 1, xb);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < 3; ++t) {
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-#pragma unroll
-          for (int m = 0; m < 4; ++m) acc[n][m] = mfma16(wf[n], (t & 1) ? xb[m] : xa[m], acc[n][m]);
-          if (t < 2) wf[n] = *reinterpret_cast<const h8*>(&wb[(t + 1) * 2048 + wo[n]]);  // next tap, same register
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (t == 0) {
-          xread(ps, dy, 2, xa);  // tap 2's X into the set tap 0 used
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        if (t < 2) {
-          dc_lgkm0();
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (dy == 2 && (u % nslab) == nslab - 1) {
-        // tile done: hi + lo + b1 -> ReLU -> . w2 over this lane's 8 channels, then the 4 lane groups
-        int bt, y0, x0;
-        tile_of(u / nslab, bt, y0, x0);
-        float bb[2][4], ww[2][4];
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            bb[n][r] = b1[n * 16 + g4 * 4 + r];
-            ww[n][r] = w2[n * 16 + g4 * 4 + r];
-          }
-        const float bias2 = b2[0];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          float part = 0.f;
-#pragma unroll
-          for (int n = 0; n < 2; ++n)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) part += fmaxf(acc[n][m][r] + acc[n + 2][m][r] + bb[n][r], 0.f) * ww[n][r];
-          part += __shfl_xor(part, 16, 64);
-          part += __shfl_xor(part, 32, 64);
-          const int y = y0 + wave * 4 + m, x = x0 + frow;
-          if (lane < 16 && y < H && x < W) depth[((long)bt * H + y) * W + x] = fmaxf(part + bias2, 0.f);
-#pragma unroll
-          for (int n = 0; n < 4; ++n) acc[n][m] = f4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      dc_wait<0>();  // W(g + 1) landed before barrier g + 1 (the depth stores drain here too)
-      (void)wnext;
-    }
-  }
-}
-
 }  // namespace
 
 #ifdef VDA_TS
@@ -712,8 +446,7 @@ extern "C" int vda_debug_dconv_timestamps(void* host) {
 }
 #endif
 
-// vda_debug_dconv (tuning build): -1 automatic (fused), 0 never, 2 resize + unfused depth conv, 3 the fused
-// conv's interpolation-wave variant
+// vda_debug_dconv (tuning build): -1 automatic (fused), 0 never, 2 resize + unfused depth conv
 VDA_KNOB(int, g_dconv_mode, -1);
 VDA_KNOB(int, g_dconv_stagger, 0);  // vda_debug_dconv_stagger
 
@@ -753,12 +486,8 @@ int vda_depth_conv_fused(const void* x, const void* w1, const float* b1, const f
   if (nt > 0x7fffffffL / 9 / ((C + 31) / 32)) return vda_set_error(-22, "depth conv: too many tiles");
   const int ntiles = (int)nt;
   const int grid = ntiles < 2 * cus ? ntiles : 2 * cus;
-  if (g_dconv_mode == 3)  // tuning build: the interpolation-wave variant
-    hipLaunchKernelGGL(depth_conv_iw_kernel, dim3(grid), dim3(64 * DCI_WAVES), 0, st, (const h16*)x, (const h16*)w1, b1,
-                       w2, b2, depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws);
-  else
-    hipLaunchKernelGGL(depth_conv_kernel<true>, dim3(grid), dim3(256), 0, st, (const h16*)x, (const h16*)w1, b1, w2, b2,
-                       depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws, (int)g_dconv_stagger);
+  hipLaunchKernelGGL(depth_conv_kernel<true>, dim3(grid), dim3(256), 0, st, (const h16*)x, (const h16*)w1, b1, w2, b2,
+                     depth, H, W, C, tiles_x, tiles_y, ntiles, Hs, Ws, (int)g_dconv_stagger);
   VDA_LAUNCH_CHECK();
   return 0;
 }
