@@ -618,7 +618,9 @@ class VideoDepthAnything(nn.Module):
         row-drop epilogue serves (vda.h drop_period), fp16, no readout."""
         if not (P.lnfold and bool(self.fold_tap_norm) and getattr(P, "projf", None) is not None):
             return False
-        return ntok >= 256 and BT * ntok >= 4096 and P.C % 64 == 0 and all(w.shape[0] % 256 == 0 for w, _, _ in P.projf)
+        M = BT * ntok
+        return (ntok >= 256 and M >= 4096 and P.C % 64 == 0 and M * P.C * 2 < 2 ** 31 and
+                all(w.shape[0] % 256 == 0 and w.numel() * 2 < 2 ** 31 for w, _, _ in P.projf))
 
     def _reassemble(self, P: _Packed, enc, BT: int, ph: int, pw: int) -> List[torch.Tensor]:
         """DPT reassemble (dpt_temporal.py:55-69 == get_motion_features :101-131, dpt.py:60-90):
